@@ -1,0 +1,113 @@
+/*
+ * libmsm — MI355X (gfx950) multi-scalar multiplication over Edwards-BLS12
+ * (ark-ed-on-bls12-377: -x^2 + y^2 = 1 + 3021 x^2 y^2 over the 253-bit BLS12-377 scalar field).
+ *
+ * C ABI that replaces the compute path under the reference's
+ *   compute_msm(baseAffinePoints, scalars) -> Promise<{x, y}>      src/submission/submission.ts:25-157
+ * i.e. the WebGPU intra-bucket reduction + Rust/wasm split / bucket-sum / window combine.
+ * Plain pointers and sizes only; every entry point is re-entrant (calls on one device serialise).
+ *
+ * Wire formats (identical to the reference's, src/submission/consts.ts:1-4, bytes.rs:11-71):
+ *   field element : 8 x uint32, BIG-endian word order (index 0 = most significant), standard form
+ *   point         : x | y | t | z  = 32 x uint32 = 128 B   (t = x*y/z, z usually 1)
+ *   scalar        : 8 x uint32 big-endian = full 256-bit integer (not reduced mod r)
+ *   result        : x | y affine = 16 x uint32; identity = (0, 1)
+ */
+#ifndef MSM_MI355X_H
+#define MSM_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Return codes.  The reference panics where these are returned (cited). */
+#define MSM_OK 0
+#define MSM_ERR_INVALID_ARG (-1)        /* null pointer / bad option                          */
+#define MSM_ERR_UNSUPPORTED_WINDOW (-2) /* lib.rs:200,208,223,231 `Unsupported window size`  */
+#define MSM_ERR_COORD_RANGE (-3)        /* bytes.rs:19 Fq::from_bigint(..).unwrap() (coord >= p) */
+#define MSM_ERR_BAD_POINT (-4)          /* z == 0 (not a projective point)                    */
+#define MSM_ERR_HIP (-5)                /* HIP runtime failure                                */
+#define MSM_ERR_NO_DEVICE (-6)          /* no gfx950 device visible: there is no CPU fallback */
+#define MSM_ERR_OOM (-7)                /* device allocation failed                           */
+
+typedef struct msm_opts {
+  uint32_t window_bits; /* 0 = auto (msm_best_window); else 4..20. Replaces ?windowSize (submission.ts:29-33) */
+  uint32_t run_length;  /* sorted-list entries per accumulation lane; 0 = auto                     */
+  int32_t device;       /* HIP device ordinal, -1 = the calling thread's current device           */
+  uint32_t flags;       /* reserved, 0                                                            */
+} msm_opts;
+
+/* Per-phase device times (ms) of the most recent MSM on the calling thread's device when
+ * profiling is enabled (hipEvents on the library's stream). */
+typedef struct msm_profile_t {
+  float prepare_points, recode_count, coarse_scan, coarse_scatter, fine_sort;
+  float accumulate, fixup, bucket_reduce_1, bucket_reduce_2, readback;
+  float device_total; /* first kernel start -> readback end */
+  float host_tail;    /* host Horner + affine conversion (wall) */
+  uint64_t entries;   /* nonzero digits sorted (= accumulation adds) */
+  uint32_t window_bits, windows, run_length, chunk_len;
+} msm_profile_t;
+
+/* Library lifetime.  msm_init replaces the wasm init()/initThreadPool (submission.ts:89-93);
+ * it probes the devices and fails with MSM_ERR_NO_DEVICE when no gfx950 is present. */
+int msm_init(void);
+void msm_shutdown(void);
+int msm_device_count(void);
+const char* msm_strerror(int code);
+
+/* getBestWindowSize (submission.ts:18-23), re-tuned for signed digits on MI355X. */
+uint32_t msm_best_window(size_t n);
+
+/* compute_msm: host-resident inputs, result on the host.  n = 0 gives the identity (0, 1),
+ * like the oracle's empty `Address.msm`. */
+int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                uint32_t out_xy_be[16]);
+
+/* Same with inputs already in device memory (device pointers, wire layout).  `hip_stream` may be
+ * NULL (library stream) or a hipStream_t to order against the caller's work. */
+int msm_compute_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                       void* hip_stream, uint32_t out_xy_be[16]);
+
+/* Shard entry for multi-GPU / co-compute: the shard's MSM as a projective point
+ * X|Y|T|Z (32 big-endian words, standard form) so shards join with one EC add each
+ * (generalises the cpu/gpu co-compute join, submission.ts:116-154 + lib.rs:240-253). */
+int msm_compute_device_partial(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n,
+                               const msm_opts* opts, void* hip_stream, uint32_t out_xyzt_be[32]);
+int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                        uint32_t out_xyzt_be[32]);
+/* Sum `count` projective partials and return the affine result. */
+int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]);
+
+/* Batch of `count` independent MSMs of equal size n, inputs contiguous ([count][n][32] points,
+ * [count][n][8] scalars), all device-resident; results [count][16].  Prover-batch shape. */
+int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
+                             const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
+
+/* point_add_affine (lib.rs:240-253): affine a + b -> affine, 16 words each. */
+int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]);
+
+/* split_dynamic (lib.rs:196-202, msm-macro lib.rs:73-177): the reference's own unsigned digit
+ * split, out[w*n + i] = c-bit window w of scalar i with w = 0 the MOST significant window,
+ * n_windows = ceil(256 / c).  Host-side; kept for interface parity and tests. */
+int msm_split(uint32_t window_bits, const uint32_t* scalars_be, size_t n, uint32_t* out);
+uint32_t msm_split_windows(uint32_t window_bits);
+
+/* Synthetic-input utilities (the benchmark page's generators, src/ui/AllBenchmarks.tsx:107-140 and
+ * src/reference/webgpu/utils.ts:81-100), host-side and multithreaded:
+ *   points_be[i] = (k0 + i*step) * G for the affine base G (16 BE words), wire layout, z = 1;
+ *   scalars_be[i] = 4 xorshift64(13,7,17) words (first = most significant) reduced mod p. */
+int msm_gen_points(const uint32_t g_xy_be[16], uint64_t k0, uint64_t step, size_t n, uint32_t* points_be);
+int msm_gen_scalars(uint64_t seed, size_t n, uint32_t* scalars_be);
+
+/* Profiling (hipEvents around every phase). */
+int msm_set_profiling(int enable);
+int msm_last_profile(msm_profile_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSM_MI355X_H */

@@ -1,0 +1,248 @@
+// Base-field arithmetic for Edwards-BLS12 on gfx950: Fq with
+//   p = 8444461749428370424248824938781546531375899335154063827935233455917409239041 (253 bits)
+// (reference: src/reference/params/AleoConstants.ts:2, src/submission/wgsl/field_modulus.wgsl:7-10).
+//
+// Representation ("fe"): 9 unsaturated limbs of 29 bits held in u32 VGPRs, Montgomery form with
+// R = 2^261.  Why not 8x32: on gfx950 v_mad_u64_u32 issues at ~4 cycles/wave but every 32-bit
+// CIOS step also needs carry adds (v_addc + VCC hazards); with 29-bit limbs a 9x9 product
+// accumulates up to 18 partial products per 64-bit column with no carry handling at all, so
+// the whole multiply is 153 independent v_mad_u64_u32 plus a short carry pass.  Measured
+// (tools/ubench/fmul_bench.hip, MI355X): 168 Gmul/s chip-wide vs 104 Gmul/s for 8x32 CIOS.
+//
+// Laziness: R = 2^261 >> p, so the Montgomery product of any a, b < 2^257 (~16p) is < 2p and
+// needs no final subtraction.  Additions are limb-wise with no carry; subtractions add a
+// redundant multiple of p whose limbs dominate any normalised limb, then renormalise.
+// Limb-size rule for fe_mul(a, b): maxlimb(a) * maxlimb(b) <= 2^60 (then each 64-bit column
+// sum <= 9*2^60 + 9*2^58 + 2^35 < 2^64).  "N" = normalised (limbs < 2^29), "S" = sum of two N
+// (limbs < 2^30).  N*N, N*S, S*S are all legal.  Values entering fe_mul stay < 2^257.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msm {
+
+constexpr int NL = 9;
+constexpr uint32_t LBITS = 29;
+constexpr uint32_t LMASK = (1u << 29) - 1;
+
+struct fe {
+  uint32_t v[NL];
+};
+
+// p in 29-bit limbs (little-endian).  p ≡ 1 (mod 2^29) so -p^-1 mod 2^29 = 2^29-1: the
+// Montgomery quotient digit is m = (-t) mod 2^29 and m*p_0 = m (no multiply).
+__device__ constexpr uint32_t P29[NL] = {1u, 277610496u, 66u, 351141280u, 452990362u,
+                                         110046747u, 358187729u, 198395284u, 1223525u};
+// R^2 mod p (to enter Montgomery form from a standard-form integer).
+__device__ constexpr uint32_t R2_29[NL] = {102099907u, 496719628u, 421467643u, 16176098u, 367912240u,
+                                           263044200u, 69768239u, 111235120u, 824440u};
+// R mod p = Montgomery form of 1.
+__device__ constexpr uint32_t ONE29[NL] = {536870474u, 276299775u, 536841777u, 282071103u, 232458597u,
+                                           117906524u, 416951824u, 75953059u, 966800u};
+// 2d*R mod p: Montgomery form of k = 2d = 6042 (add-2008-hwcd-3's constant).
+__device__ constexpr uint32_t K2D29[NL] = {534219742u, 493355007u, 360522798u, 7852223u, 582682u,
+                                           196969042u, 170238326u, 321828089u, 296340u};
+// 2d*R^2 mod p: fe_mul(t_std, K2D_R2) = Montgomery form of 2d*t straight from standard form.
+__device__ constexpr uint32_t K2D_R2_29[NL] = {22956135u, 32535989u, 128498189u, 216570651u, 307994937u,
+                                               462062068u, 55188476u, 243732681u, 295952u};
+// 8p in a redundant form with limbs 0..7 >= 2^29-1, so (a + K8P - b) never goes negative limb-wise
+// for normalised b.
+__device__ constexpr uint32_t K8P29[NL] = {536870920u, 610271231u, 536871443u, 661646591u, 939568340u,
+                                           880373981u, 718018184u, 1050291364u, 9788201u};
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * b + c;
+}
+
+__device__ __forceinline__ void fe_set(fe& r, const uint32_t* c) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c[i];
+}
+__device__ __forceinline__ fe fe_const(const uint32_t* c) {
+  fe r;
+  fe_set(r, c);
+  return r;
+}
+__device__ __forceinline__ fe fe_zero() {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = 0;
+  return r;
+}
+__device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
+
+// Montgomery product a*b*2^-261 mod p (result normalised, value < 2p when a,b < 2^257).
+__device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
+  uint64_t c[2 * NL];
+#pragma unroll
+  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++)
+#pragma unroll
+    for (int j = 0; j < NL; j++) c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    uint32_t m = (0u - (uint32_t)c[i]) & LMASK;
+    c[i] += m;  // m * p_0, p_0 == 1: low 29 bits of c[i] become zero
+    c[i + 1] += c[i] >> LBITS;
+#pragma unroll
+    for (int j = 1; j < NL; j++) c[i + j] = mad64(m, P29[j], c[i + j]);
+  }
+  fe r;
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    c[k + 1] += c[k] >> LBITS;
+    r.v[k - NL] = (uint32_t)c[k] & LMASK;
+  }
+  r.v[NL - 1] = (uint32_t)c[2 * NL - 1];
+  return r;
+}
+
+__device__ __forceinline__ fe fe_sqr(const fe& a) { return fe_mul(a, a); }
+
+// Carry-propagate so limbs 0..7 are < 2^29 (value unchanged).
+__device__ __forceinline__ void fe_norm(fe& a) {
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    a.v[i + 1] += a.v[i] >> LBITS;
+    a.v[i] &= LMASK;
+  }
+}
+
+// Lazy add: limb-wise, no carry (N+N -> S).
+__device__ __forceinline__ fe fe_add(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+// a + b, normalised.
+__device__ __forceinline__ fe fe_add_n(const fe& a, const fe& b) {
+  fe r = fe_add(a, b);
+  fe_norm(r);
+  return r;
+}
+// a + a, normalised.
+__device__ __forceinline__ fe fe_dbl_n(const fe& a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] << 1;
+  fe_norm(r);
+  return r;
+}
+// a - b + 8p, normalised.  Requires b normalised with value < 8p; a limbs < 2^30.
+__device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + K8P29[i] - b.v[i];
+  fe_norm(r);
+  return r;
+}
+// -b (= 8p - b), normalised.
+__device__ __forceinline__ fe fe_neg(const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = K8P29[i] - b.v[i];
+  fe_norm(r);
+  return r;
+}
+// Branch-free select: c ? b : a.
+__device__ __forceinline__ fe fe_sel(bool c, const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c ? b.v[i] : a.v[i];
+  return r;
+}
+
+// Standard-form little-endian 8x32 word integer (< 2^256) -> 29-bit limbs (not Montgomery).
+__device__ __forceinline__ fe fe_from_words_le(const uint32_t w[8]) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+    uint32_t lo = w[wi] >> sh;
+    uint32_t hi = (sh > 3 && wi + 1 < 8) ? (w[wi + 1] << (32 - sh)) : 0u;
+    r.v[i] = (lo | hi) & LMASK;
+  }
+  return r;
+}
+
+// Normalised limbs (value < 2^261) -> little-endian 8x32 words (value must be < 2^256).
+__device__ __forceinline__ void fe_to_words_le(const fe& a, uint32_t w[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+    w[wi] |= a.v[i] << sh;
+    if (sh > 3 && wi + 1 < 8) w[wi + 1] |= a.v[i] >> (32 - sh);
+  }
+}
+
+// Compare normalised limbs (value < 2^261) against p: returns true if a >= p.
+__device__ __forceinline__ bool fe_geq_p(const fe& a) {
+  bool gt = false, eq = true;
+#pragma unroll
+  for (int i = NL - 1; i >= 0; i--) {
+    bool g = a.v[i] > P29[i], l = a.v[i] < P29[i];
+    gt = gt || (eq && g);
+    eq = eq && !g && !l;
+  }
+  return gt || eq;
+}
+
+// a - p for normalised a >= p (result normalised; borrows handled limb-wise).
+__device__ __forceinline__ fe fe_sub_p(const fe& a) {
+  fe r;
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    int64_t t = (int64_t)a.v[i] - P29[i] + borrow;
+    borrow = t < 0 ? -1 : 0;
+    r.v[i] = (uint32_t)(t + (t < 0 ? (1ll << 29) : 0));
+  }
+  return r;
+}
+
+// Montgomery form -> canonical standard form in [0, p) as normalised limbs.
+__device__ __forceinline__ fe fe_to_std(const fe& a) {
+  fe one = fe_zero();
+  one.v[0] = 1;
+  fe r = fe_mul(a, one);  // value <= p
+  fe_norm(r);
+  if (fe_geq_p(r)) r = fe_sub_p(r);
+  return r;
+}
+
+// Standard-form words (< 2^256) -> Montgomery form (normalised, < 2p).
+__device__ __forceinline__ fe fe_to_mont(const fe& std_limbs) { return fe_mul(std_limbs, fe_const(R2_29)); }
+
+// Check a standard-form 256-bit value (LE words) is < p.
+__device__ __forceinline__ bool words_lt_p(const uint32_t w[8]) {
+  const uint32_t PW[8] = {0x00000001u, 0x0a118000u, 0xd0000001u, 0x59aa76feu,
+                          0x5c37b001u, 0x60b44d1eu, 0x9a2ca556u, 0x12ab655eu};
+  bool lt = false, eq = true;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    lt = lt || (eq && w[i] < PW[i]);
+    eq = eq && (w[i] == PW[i]);
+  }
+  return lt;
+}
+
+// Inverse by Fermat (a^(p-2)); only used on the rare z != 1 input path.
+__device__ inline fe fe_inv(const fe& a) {
+  // p - 2 as little-endian words
+  const uint32_t E[8] = {0xffffffffu, 0x0a117fffu, 0xd0000001u, 0x59aa76feu,
+                         0x5c37b001u, 0x60b44d1eu, 0x9a2ca556u, 0x12ab655eu};
+  fe r = fe_one();
+  for (int wi = 7; wi >= 0; wi--) {
+    for (int b = 31; b >= 0; b--) {
+      r = fe_sqr(r);
+      if ((E[wi] >> b) & 1u) r = fe_mul(r, a);
+    }
+  }
+  return r;
+}
+
+}  // namespace msm

@@ -1,0 +1,701 @@
+// libmsm host driver: C ABI (include/msm.h), device workspaces, launch sequence, host tail.
+//
+// The reference's host orchestration this replaces:
+//   compute_msm            src/submission/submission.ts:25-157   -> msm_compute / msm_compute_device
+//   getBestWindowSize      submission.ts:18-23                    -> msm_best_window
+//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_fixup
+//   split_dynamic          msm-wasm/src/lib.rs:196-202            -> msm_split (host) / k_recode_* (device)
+//   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1/2
+//   reduce_last            lib.rs:88-104                          -> horner_tail (host)
+//   point_add_affine       lib.rs:240-253                         -> msm_point_add_affine
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/msm.h"
+#include "hostfield.h"
+#include "msm_util.h"
+#include "msm_kernels.hip"
+
+using namespace msm;
+using namespace msmh;
+
+namespace {
+
+#define HIPCHECK(expr)                                                                         \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) {                                                                    \
+      fprintf(stderr, "libmsm: HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return _e == hipErrorOutOfMemory ? MSM_ERR_OOM : MSM_ERR_HIP;                            \
+    }                                                                                          \
+  } while (0)
+
+enum Phase {
+  PH_START = 0,
+  PH_PREPARE,
+  PH_RECODE,
+  PH_SCAN,
+  PH_SCATTER,
+  PH_FINE,
+  PH_ACCUM,
+  PH_FIXUP,
+  PH_RED1,
+  PH_RED2,
+  PH_READBACK,
+  PH_COUNT
+};
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return MSM_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return MSM_ERR_OOM;
+    }
+    cap = want;
+    return MSM_OK;
+  }
+  template <typename T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return MSM_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return MSM_ERR_OOM;
+    }
+    cap = bytes;
+    return MSM_OK;
+  }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct DevCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  Buf wire_points, wire_scalars, pts, err, coarse_count, coarse_base, coarse_cursor;
+  Buf part_entry, part_fine, sorted_entry, sorted_key, bucket_count, buckets;
+  Buf run_head, run_tail, head_key, tail_key, red_U, red_T, red_out;
+  HostBuf h_out;
+  hipEvent_t ev[PH_COUNT] = {};
+  bool profiling = false;
+  msm_profile_t last{};
+};
+
+std::mutex g_mu;
+std::vector<DevCtx*> g_ctx;
+bool g_profiling = false;
+int g_ndev = -1;
+
+int probe_devices() {
+  if (g_ndev >= 0) return g_ndev;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  int good = 0;
+  for (int i = 0; i < n; i++) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) good++;
+  }
+  g_ndev = good == n ? n : good;
+  return g_ndev;
+}
+
+int get_ctx(int device, DevCtx** out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (probe_devices() <= 0) return MSM_ERR_NO_DEVICE;
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) return MSM_ERR_HIP;
+  }
+  if (device >= g_ndev) return MSM_ERR_INVALID_ARG;
+  if ((int)g_ctx.size() < g_ndev) g_ctx.resize(g_ndev, nullptr);
+  if (!g_ctx[device]) {
+    DevCtx* c = new DevCtx();
+    c->device = device;
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) {
+      delete c;
+      return MSM_ERR_HIP;
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      hipSetDevice(prev);
+      return MSM_ERR_HIP;
+    }
+    for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
+    hipSetDevice(prev);
+    g_ctx[device] = c;
+  }
+  g_ctx[device]->profiling = g_profiling;
+  *out = g_ctx[device];
+  return MSM_OK;
+}
+
+struct Plan {
+  MsmDims d;
+  uint32_t K;       // run length
+  uint32_t L;       // bucket-reduce chunk length
+  uint32_t lgL;
+  uint32_t nchunks; // B / L
+  uint32_t nterms;  // 1 + log2(nchunks)
+  size_t Mmax;      // W * n upper bound on sorted entries
+  size_t runs_max;
+};
+
+uint32_t ilog2(uint32_t v) {
+  uint32_t r = 0;
+  while ((1u << (r + 1)) <= v) r++;
+  return r;
+}
+
+int make_plan(size_t n, const msm_opts* o, Plan* pl) {
+  uint32_t c = (o && o->window_bits) ? o->window_bits : msm_best_window(n);
+  if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
+  if (n >= (1ull << 30)) return MSM_ERR_INVALID_ARG;
+  MsmDims d;
+  d.n = (uint32_t)n;
+  d.c = c;
+  d.B = 1u << (c - 1);
+  d.W = (257 + c - 1) / c;
+  d.fb = std::min<uint32_t>(c - 1, 9);
+  d.nbc = d.B >> d.fb;
+  d.nbins = d.W * d.nbc;
+  d.spt = 16;
+  pl->d = d;
+  pl->K = (o && o->run_length) ? o->run_length : 32;
+  if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
+  pl->L = std::min<uint32_t>(8, d.B);
+  pl->lgL = ilog2(pl->L);
+  pl->nchunks = d.B / pl->L;
+  pl->nterms = 1 + ilog2(pl->nchunks);
+  pl->Mmax = (size_t)d.W * n;
+  pl->runs_max = (pl->Mmax + pl->K - 1) / pl->K + 1;
+  if (pl->Mmax >= (1ull << 31)) return MSM_ERR_INVALID_ARG;
+  return MSM_OK;
+}
+
+int ensure_workspace(DevCtx* c, const Plan& pl) {
+  const MsmDims& d = pl.d;
+  const size_t nb = (size_t)d.W * d.B;
+  int rc;
+#define ENS(buf, bytes) \
+  if ((rc = c->buf.ensure(bytes)) != MSM_OK) return rc
+  ENS(pts, (size_t)d.n * PRE_WORDS * 4);
+  ENS(err, 16);
+  ENS(coarse_count, (size_t)d.nbins * 4);
+  ENS(coarse_base, ((size_t)d.nbins + 1) * 4);
+  ENS(coarse_cursor, (size_t)d.nbins * 4);
+  ENS(part_entry, pl.Mmax * 4);
+  ENS(part_fine, pl.Mmax * 2);
+  ENS(sorted_entry, pl.Mmax * 4);
+  ENS(sorted_key, pl.Mmax * 4);
+  ENS(bucket_count, nb * 4);
+  ENS(buckets, nb * PT_WORDS * 4);
+  ENS(run_head, pl.runs_max * PT_WORDS * 4);
+  ENS(run_tail, pl.runs_max * PT_WORDS * 4);
+  ENS(head_key, pl.runs_max * 4);
+  ENS(tail_key, pl.runs_max * 4);
+  ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
+  ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
+  ENS(red_out, (size_t)d.W * pl.nterms * 32 * 4 + 64);
+#undef ENS
+  if ((rc = c->h_out.ensure((size_t)d.W * pl.nterms * 32 * 4 + 64)) != MSM_OK) return rc;
+  return MSM_OK;
+}
+
+inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
+
+// Enqueue the whole device pipeline on `s`; the reduced per-window terms land in c->h_out.
+int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s) {
+  const MsmDims& d = pl.d;
+  const bool prof = c->profiling;
+  auto mark = [&](int ph) {
+    if (prof) hipEventRecord(c->ev[ph], s);
+  };
+  mark(PH_START);
+  HIPCHECK(hipMemsetAsync(c->err.p, 0, 16, s));
+  HIPCHECK(hipMemsetAsync(c->coarse_count.p, 0, (size_t)d.nbins * 4, s));
+  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
+                     c->err.as<uint32_t>());
+  mark(PH_PREPARE);
+  const unsigned sgrid = grid_for(d.n, 256 * d.spt);
+  const size_t lds = (size_t)d.nbins * 4;
+  hipLaunchKernelGGL(k_recode_count, dim3(sgrid), dim3(256), lds, s, d_scalars, d, c->coarse_count.as<uint32_t>());
+  mark(PH_RECODE);
+  hipLaunchKernelGGL(k_coarse_scan, dim3(1), dim3(1024), 0, s, c->coarse_count.as<uint32_t>(),
+                     c->coarse_base.as<uint32_t>(), c->coarse_cursor.as<uint32_t>(), d.nbins);
+  mark(PH_SCAN);
+  hipLaunchKernelGGL(k_coarse_scatter, dim3(sgrid), dim3(256), lds, s, d_scalars, d, c->coarse_cursor.as<uint32_t>(),
+                     c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+  mark(PH_SCATTER);
+  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(256), 0, s, c->part_entry.as<uint32_t>(),
+                     c->part_fine.as<uint16_t>(), c->coarse_base.as<uint32_t>(), d, c->sorted_entry.as<uint32_t>(),
+                     c->sorted_key.as<uint32_t>(), c->bucket_count.as<uint32_t>());
+  mark(PH_FINE);
+  const uint32_t* total = c->coarse_base.as<uint32_t>() + d.nbins;
+  const unsigned rgrid = grid_for(pl.runs_max, 256);
+  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(256), 0, s, c->pts.as<uint32_t>(), c->sorted_entry.as<uint32_t>(),
+                     c->sorted_key.as<uint32_t>(), total, pl.K, c->buckets.as<uint32_t>(), c->run_head.as<uint32_t>(),
+                     c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(), c->tail_key.as<uint32_t>());
+  mark(PH_ACCUM);
+  hipLaunchKernelGGL(k_fixup, dim3(rgrid), dim3(256), 0, s, total, pl.K, c->run_head.as<uint32_t>(),
+                     c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(), c->tail_key.as<uint32_t>(),
+                     c->buckets.as<uint32_t>());
+  mark(PH_FIXUP);
+  hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
+                     c->buckets.as<uint32_t>(), c->bucket_count.as<uint32_t>(), d, pl.L, c->red_U.as<uint32_t>(),
+                     c->red_T.as<uint32_t>());
+  mark(PH_RED1);
+  hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, c->red_U.as<uint32_t>(),
+                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nterms, c->red_out.as<uint32_t>());
+  mark(PH_RED2);
+  HIPCHECK(hipGetLastError());
+  const size_t outb = (size_t)d.W * pl.nterms * 32 * 4;
+  HIPCHECK(hipMemcpyAsync(c->h_out.p, c->red_out.p, outb, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync((char*)c->h_out.p + outb, c->err.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync((char*)c->h_out.p + outb + 4, total, 4, hipMemcpyDeviceToHost, s));
+  mark(PH_READBACK);
+  return MSM_OK;
+}
+
+// Host tail: MSM = sum_w 2^(c w) [ R_{w,V} + sum_k 2^(lgL + k) R_{w,k} ]  (Horner over bit positions).
+// Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then into_affine.
+Pt horner_tail(const Plan& pl, const uint32_t* terms) {
+  const MsmDims& d = pl.d;
+  const uint32_t maxpos = d.c * (d.W - 1) + pl.lgL + (pl.nterms - 1);
+  std::vector<std::vector<Pt>> at(maxpos + 1);
+  for (uint32_t w = 0; w < d.W; w++) {
+    for (uint32_t t = 0; t < pl.nterms; t++) {
+      const uint32_t* o = terms + ((size_t)w * pl.nterms + t) * 32;
+      Pt p;
+      p.X = fq_from_std(reinterpret_cast<const uint64_t*>(o));
+      p.Y = fq_from_std(reinterpret_cast<const uint64_t*>(o + 8));
+      p.T = fq_from_std(reinterpret_cast<const uint64_t*>(o + 16));
+      p.Z = fq_from_std(reinterpret_cast<const uint64_t*>(o + 24));
+      if (fq_is_zero(p.X) && fq_eq(p.Y, p.Z)) continue;  // identity
+      uint32_t pos = d.c * w + (t == 0 ? 0 : pl.lgL + (t - 1));
+      at[pos].push_back(p);
+    }
+  }
+  Pt acc = pt_identity();
+  bool live = false;
+  for (int pos = (int)maxpos; pos >= 0; pos--) {
+    if (live) acc = pt_dbl(acc);
+    for (const Pt& p : at[pos]) {
+      acc = live ? pt_add(acc, p) : p;
+      live = true;
+    }
+  }
+  return acc;
+}
+
+void pt_to_be_affine(const Pt& p, uint32_t out[16]) {
+  uint64_t x[4], y[4];
+  pt_to_affine_std(p, x, y);
+  std_to_be_words(x, out);
+  std_to_be_words(y, out + 8);
+}
+void pt_to_be_xyzt(const Pt& p, uint32_t out[32]) {
+  uint64_t s[4];
+  const Fq* f[4] = {&p.X, &p.Y, &p.T, &p.Z};
+  for (int i = 0; i < 4; i++) {
+    fq_to_std(*f[i], s);
+    std_to_be_words(s, out + 8 * i);
+  }
+}
+int pt_from_be_xyzt(const uint32_t in[32], Pt* p) {
+  uint64_t s[4];
+  Fq* f[4] = {&p->X, &p->Y, &p->T, &p->Z};
+  for (int i = 0; i < 4; i++) {
+    be_words_to_std(in + 8 * i, s);
+    if (!std_lt_p(s)) return MSM_ERR_COORD_RANGE;
+    *f[i] = fq_from_std(s);
+  }
+  return MSM_OK;
+}
+
+using clk = std::chrono::steady_clock;
+
+// Run one MSM with device inputs; result as a projective host point.
+int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, size_t n, const msm_opts* o,
+               hipStream_t user_stream, Pt* result) {
+  if (n == 0) {
+    *result = pt_identity();
+    return MSM_OK;
+  }
+  Plan pl;
+  int rc = make_plan(n, o, &pl);
+  if (rc != MSM_OK) return rc;
+  if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
+  hipStream_t s = user_stream ? user_stream : c->stream;
+  if ((rc = enqueue_msm(c, pl, d_points, d_scalars, s)) != MSM_OK) return rc;
+  HIPCHECK(hipStreamSynchronize(s));
+  const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(c->h_out.p);
+  uint32_t err = h[outb / 4];
+  uint32_t total = h[outb / 4 + 1];
+  if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
+  if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
+  auto t0 = clk::now();
+  *result = horner_tail(pl, h);
+  auto t1 = clk::now();
+  if (c->profiling) {
+    float ms[PH_COUNT] = {};
+    for (int i = 1; i < PH_COUNT; i++) hipEventElapsedTime(&ms[i], c->ev[i - 1], c->ev[i]);
+    msm_profile_t& P = c->last;
+    P.prepare_points = ms[PH_PREPARE];
+    P.recode_count = ms[PH_RECODE];
+    P.coarse_scan = ms[PH_SCAN];
+    P.coarse_scatter = ms[PH_SCATTER];
+    P.fine_sort = ms[PH_FINE];
+    P.accumulate = ms[PH_ACCUM];
+    P.fixup = ms[PH_FIXUP];
+    P.bucket_reduce_1 = ms[PH_RED1];
+    P.bucket_reduce_2 = ms[PH_RED2];
+    P.readback = ms[PH_READBACK];
+    hipEventElapsedTime(&P.device_total, c->ev[PH_START], c->ev[PH_READBACK]);
+    P.host_tail = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    P.entries = total;
+    P.window_bits = pl.d.c;
+    P.windows = pl.d.W;
+    P.run_length = pl.K;
+    P.chunk_len = pl.L;
+  }
+  return MSM_OK;
+}
+
+int with_device(const msm_opts* o, DevCtx** c) {
+  int dev = o ? o->device : -1;
+  return get_ctx(dev, c);
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+int run_host(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts, Pt* result) {
+  DevCtx* c;
+  int rc = with_device(opts, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (n == 0) {
+    *result = pt_identity();
+    return MSM_OK;
+  }
+  if ((rc = c->wire_points.ensure(n * 128)) != MSM_OK) return rc;
+  if ((rc = c->wire_scalars.ensure(n * 32)) != MSM_OK) return rc;
+  HIPCHECK(hipMemcpyAsync(c->wire_points.p, points_be, n * 128, hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(hipMemcpyAsync(c->wire_scalars.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
+  return run_device(c, c->wire_points.as<uint32_t>(), c->wire_scalars.as<uint32_t>(), n, opts, nullptr, result);
+}
+
+}  // namespace
+
+extern "C" {
+
+int msm_init(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return probe_devices() > 0 ? MSM_OK : MSM_ERR_NO_DEVICE;
+}
+
+void msm_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (DevCtx* c : g_ctx) {
+    if (!c) continue;
+    std::lock_guard<std::mutex> lk2(c->mu);
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->coarse_count, &c->coarse_base,
+                   &c->coarse_cursor, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->sorted_key,
+                   &c->bucket_count, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_key,
+                   &c->red_U, &c->red_T, &c->red_out};
+    for (Buf* b : bufs) b->release();
+    c->h_out.release();
+    for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
+    hipStreamDestroy(c->stream);
+    hipSetDevice(prev);
+  }
+  for (DevCtx*& c : g_ctx) {
+    delete c;
+    c = nullptr;
+  }
+}
+
+int msm_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return probe_devices();
+}
+
+const char* msm_strerror(int code) {
+  switch (code) {
+    case MSM_OK: return "ok";
+    case MSM_ERR_INVALID_ARG: return "invalid argument";
+    case MSM_ERR_UNSUPPORTED_WINDOW: return "unsupported window size";
+    case MSM_ERR_COORD_RANGE: return "coordinate not in [0, p)";
+    case MSM_ERR_BAD_POINT: return "invalid point (z == 0)";
+    case MSM_ERR_HIP: return "HIP runtime error";
+    case MSM_ERR_NO_DEVICE: return "no gfx950 (MI355X) device available";
+    case MSM_ERR_OOM: return "device out of memory";
+    default: return "unknown error";
+  }
+}
+
+uint32_t msm_best_window(size_t n) {
+  // Signed digits: cost ~ W*n (accumulation) + ~2*W*2^(c-1) (bucket running sums) weighted by
+  // the reduction's lower parallelism.  Pick the minimum over c in [8, 16].
+  if (n == 0) return 8;
+  double best = 1e300;
+  uint32_t bc = 8;
+  for (uint32_t c = 8; c <= 16; c++) {
+    double W = (257.0 + c - 1) / c;
+    W = (double)(uint32_t)W;
+    double cost = W * (double)n + 3.0 * W * (double)(1u << (c - 1));
+    if (cost < best) {
+      best = cost;
+      bc = c;
+    }
+  }
+  return bc;
+}
+
+int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                uint32_t out_xy_be[16]) {
+  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  if (!out_xy_be) return MSM_ERR_INVALID_ARG;
+  Pt r;
+  int rc = run_host(points_be, scalars_be, n, opts, &r);
+  if (rc != MSM_OK) return rc;
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
+int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                        uint32_t out_xyzt_be[32]) {
+  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;
+  Pt r;
+  int rc = run_host(points_be, scalars_be, n, opts, &r);
+  if (rc != MSM_OK) return rc;
+  pt_to_be_xyzt(r, out_xyzt_be);
+  return MSM_OK;
+}
+
+static int device_entry(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                        void* hip_stream, Pt* r) {
+  if ((!d_points_be || !d_scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  DevCtx* c;
+  int rc = with_device(opts, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return run_device(c, d_points_be, d_scalars_be, n, opts, (hipStream_t)hip_stream, r);
+}
+
+int msm_compute_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                       void* hip_stream, uint32_t out_xy_be[16]) {
+  if (!out_xy_be) return MSM_ERR_INVALID_ARG;
+  Pt r;
+  int rc = device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
+  if (rc != MSM_OK) return rc;
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
+int msm_compute_device_partial(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n,
+                               const msm_opts* opts, void* hip_stream, uint32_t out_xyzt_be[32]) {
+  if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;
+  Pt r;
+  int rc = device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
+  if (rc != MSM_OK) return rc;
+  pt_to_be_xyzt(r, out_xyzt_be);
+  return MSM_OK;
+}
+
+int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
+                             const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be) {
+  if (!out_xy_be || ((!d_points_be || !d_scalars_be) && n && count)) return MSM_ERR_INVALID_ARG;
+  for (size_t b = 0; b < count; b++) {
+    int rc = msm_compute_device(d_points_be + b * n * 32, d_scalars_be + b * n * 8, n, opts, hip_stream,
+                                out_xy_be + 16 * b);
+    if (rc != MSM_OK) return rc;
+  }
+  return MSM_OK;
+}
+
+int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]) {
+  if ((!partials_xyzt_be && count) || !out_xy_be) return MSM_ERR_INVALID_ARG;
+  Pt acc = pt_identity();
+  for (size_t i = 0; i < count; i++) {
+    Pt p;
+    int rc = pt_from_be_xyzt(partials_xyzt_be + 32 * i, &p);
+    if (rc != MSM_OK) return rc;
+    if (fq_is_zero(p.Z)) return MSM_ERR_BAD_POINT;
+    acc = pt_add(acc, p);
+  }
+  pt_to_be_affine(acc, out_xy_be);
+  return MSM_OK;
+}
+
+int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]) {
+  if (!a_xy_be || !b_xy_be || !out_xy_be) return MSM_ERR_INVALID_ARG;
+  uint64_t ax[4], ay[4], bx[4], by[4];
+  be_words_to_std(a_xy_be, ax);
+  be_words_to_std(a_xy_be + 8, ay);
+  be_words_to_std(b_xy_be, bx);
+  be_words_to_std(b_xy_be + 8, by);
+  if (!std_lt_p(ax) || !std_lt_p(ay) || !std_lt_p(bx) || !std_lt_p(by)) return MSM_ERR_COORD_RANGE;
+  Pt r = pt_add(pt_from_affine_std(ax, ay), pt_from_affine_std(bx, by));
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
+uint32_t msm_split_windows(uint32_t window_bits) {
+  if (window_bits == 0 || window_bits > 32) return 0;
+  return (256 + window_bits - 1) / window_bits;
+}
+
+int msm_split(uint32_t c, const uint32_t* scalars_be, size_t n, uint32_t* out) {
+  // Reference semantics (msm-macro/src/lib.rs:90-176): window i (0 = least significant) takes bits
+  // [c*i, c*i + c) of the big-endian u32[8] scalar; output index j = n_windows - 1 - i (MSB first).
+  if (c == 0 || c > 31) return MSM_ERR_UNSUPPORTED_WINDOW;
+  if ((!scalars_be || !out) && n) return MSM_ERR_INVALID_ARG;
+  const uint32_t nw = msm_split_windows(c);
+  for (size_t s = 0; s < n; s++) {
+    const uint32_t* be = scalars_be + 8 * s;
+    for (uint32_t i = 0; i < nw; i++) {
+      uint32_t bit = c * i, v = 0;
+      for (uint32_t b = 0; b < c && bit + b < 256; b++) {
+        uint32_t pos = bit + b;
+        uint32_t word = be[7 - pos / 32];
+        v |= ((word >> (pos % 32)) & 1u) << b;
+      }
+      out[(size_t)(nw - 1 - i) * n + s] = v;
+    }
+  }
+  return MSM_OK;
+}
+
+int msm_set_profiling(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_profiling = enable != 0;
+  for (DevCtx* c : g_ctx)
+    if (c) c->profiling = g_profiling;
+  return MSM_OK;
+}
+
+int msm_last_profile(msm_profile_t* out) {
+  if (!out) return MSM_ERR_INVALID_ARG;
+  DevCtx* c;
+  int rc = get_ctx(-1, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = c->last;
+  return MSM_OK;
+}
+
+int msm_gen_points(const uint32_t g_xy_be[16], uint64_t k0, uint64_t step, size_t n, uint32_t* points_be) {
+  if (!g_xy_be || (!points_be && n)) return MSM_ERR_INVALID_ARG;
+  uint64_t gx[4], gy[4];
+  be_words_to_std(g_xy_be, gx);
+  be_words_to_std(g_xy_be + 8, gy);
+  if (!std_lt_p(gx) || !std_lt_p(gy)) return MSM_ERR_COORD_RANGE;
+  gen_points(pt_from_affine_std(gx, gy), k0, step, n, points_be);
+  return MSM_OK;
+}
+
+int msm_gen_scalars(uint64_t seed, size_t n, uint32_t* scalars_be) {
+  if (!scalars_be && n) return MSM_ERR_INVALID_ARG;
+  gen_scalars(seed, n, scalars_be);
+  return MSM_OK;
+}
+
+// ---- test hooks (not in msm.h): batch field / point ops on the device, canonical LE words ----
+int msm_test_field_op(uint32_t op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
+  DevCtx* c;
+  int rc = get_ctx(-1, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  uint32_t *da, *db, *dout;
+  HIPCHECK(hipMalloc(&da, n * 32 + 32));
+  HIPCHECK(hipMalloc(&db, n * 32 + 32));
+  HIPCHECK(hipMalloc(&dout, n * 32 + 32));
+  HIPCHECK(hipMemcpy(da, a, n * 32, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(db, b, n * 32, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_test_field, dim3(grid_for(n, 256)), dim3(256), 0, 0, da, db, dout, (uint32_t)n, op);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpy(out, dout, n * 32, hipMemcpyDeviceToHost));
+  hipFree(da);
+  hipFree(db);
+  hipFree(dout);
+  return MSM_OK;
+}
+
+int msm_test_point_op(uint32_t op, const uint32_t* p, const uint32_t* q, uint32_t* out, size_t n) {
+  DevCtx* c;
+  int rc = get_ctx(-1, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  uint32_t *dp, *dq, *dout;
+  HIPCHECK(hipMalloc(&dp, n * 64 + 64));
+  HIPCHECK(hipMalloc(&dq, n * 64 + 64));
+  HIPCHECK(hipMalloc(&dout, n * 128 + 128));
+  HIPCHECK(hipMemcpy(dp, p, n * 64, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dq, q, n * 64, hipMemcpyHostToDevice));
+  if (op == 0)
+    hipLaunchKernelGGL(k_test_point<0>, dim3(grid_for(n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);
+  else if (op == 1)
+    hipLaunchKernelGGL(k_test_point<1>, dim3(grid_for(n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);
+  else
+    hipLaunchKernelGGL(k_test_point<2>, dim3(grid_for(n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpy(out, dout, n * 128, hipMemcpyDeviceToHost));
+  hipFree(dp);
+  hipFree(dq);
+  hipFree(dout);
+  return MSM_OK;
+}
+
+}  // extern "C"

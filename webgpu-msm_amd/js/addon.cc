@@ -1,0 +1,279 @@
+// Node N-API addon: the thin FFI between the reference's TypeScript surface
+// (compute_msm, src/submission/submission.ts:25-157) and libmsm's C ABI (include/msm.h).
+//
+// Exports (all compute is asynchronous through napi_async_work, resolving a Promise, because
+// compute_msm is async in the reference):
+//   computeMsmU32(points: Uint32Array(32n), scalars: Uint32Array(8n), windowSize) -> Promise<Uint32Array(16)>
+//   computeMsmBigInt(points: {x,y,t,z: bigint}[], scalars: bigint[], windowSize) -> Promise<Uint32Array(16)>
+//       BigInt -> big-endian u32 marshalling happens natively (napi_get_value_bigint_words),
+//       replacing convert_worker.ts:8-57 and the 8-worker fan-out of submission.ts:47-74.
+//   pointAddAffine(a: Uint32Array(16), b: Uint32Array(16)) -> Uint32Array(16)      (lib.rs:240-253)
+//   split(windowSize, scalars: Uint32Array(8n)) -> Uint32Array(W*n)                 (lib.rs:196-202)
+//   bestWindowSize(n) -> number                                                     (submission.ts:18-23)
+//   init() -> number (0 ok), deviceCount() -> number, strerror(code) -> string
+#include <node_api.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "msm.h"
+
+namespace {
+
+#define NAPI_OK(call)                                              \
+  do {                                                             \
+    if ((call) != napi_ok) {                                       \
+      napi_throw_error(env, nullptr, "N-API call failed: " #call); \
+      return nullptr;                                              \
+    }                                                              \
+  } while (0)
+
+struct Job {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  std::vector<uint32_t> points, scalars;
+  size_t n = 0;
+  uint32_t window = 0;
+  uint32_t out[16] = {0};
+  int rc = 0;
+};
+
+void execute(napi_env, void* data) {
+  Job* j = static_cast<Job*>(data);
+  msm_opts o;
+  memset(&o, 0, sizeof(o));
+  o.window_bits = j->window;
+  o.device = -1;
+  j->rc = msm_compute(j->points.data(), j->scalars.data(), j->n, &o, j->out);
+}
+
+void complete(napi_env env, napi_status, void* data) {
+  Job* j = static_cast<Job*>(data);
+  if (j->rc == MSM_OK) {
+    napi_value ab, arr;
+    void* buf;
+    napi_create_arraybuffer(env, 64, &buf, &ab);
+    memcpy(buf, j->out, 64);
+    napi_create_typedarray(env, napi_uint32_array, 16, ab, 0, &arr);
+    napi_resolve_deferred(env, j->deferred, arr);
+  } else {
+    napi_value msg, code, err;
+    std::string m = std::string("libmsm: ") + msm_strerror(j->rc);
+    napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
+    napi_create_int32(env, j->rc, &code);
+    napi_create_error(env, nullptr, msg, &err);
+    napi_set_named_property(env, err, "code", code);
+    napi_reject_deferred(env, j->deferred, err);
+  }
+  napi_delete_async_work(env, j->work);
+  delete j;
+}
+
+napi_value start_job(napi_env env, Job* j) {
+  napi_value promise, name;
+  NAPI_OK(napi_create_promise(env, &j->deferred, &promise));
+  NAPI_OK(napi_create_string_utf8(env, "msm_compute", NAPI_AUTO_LENGTH, &name));
+  NAPI_OK(napi_create_async_work(env, nullptr, name, execute, complete, j, &j->work));
+  NAPI_OK(napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+bool get_u32_array(napi_env env, napi_value v, const uint32_t** data, size_t* len) {
+  bool is_ta = false;
+  if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return false;
+  napi_typedarray_type t;
+  void* d;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, len, &d, &ab, &off) != napi_ok || t != napi_uint32_array) return false;
+  *data = static_cast<const uint32_t*>(d);
+  return true;
+}
+
+uint32_t get_window(napi_env env, napi_value v) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_number) return 0;
+  uint32_t w = 0;
+  napi_get_value_uint32(env, v, &w);
+  return w;
+}
+
+napi_value ComputeMsmU32(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint32_t *pts, *sc;
+  size_t plen, slen;
+  if (argc < 2 || !get_u32_array(env, argv[0], &pts, &plen) || !get_u32_array(env, argv[1], &sc, &slen)) {
+    napi_throw_type_error(env, nullptr, "computeMsmU32(points: Uint32Array, scalars: Uint32Array, windowSize?)");
+    return nullptr;
+  }
+  Job* j = new Job();
+  j->n = std::min(plen / 32, slen / 8);
+  j->points.assign(pts, pts + j->n * 32);
+  j->scalars.assign(sc, sc + j->n * 8);
+  j->window = argc > 2 ? get_window(env, argv[2]) : 0;
+  return start_job(env, j);
+}
+
+// bigint -> 8 big-endian u32 words; false if negative or wider than 256 bits
+bool bigint_be(napi_env env, napi_value v, uint32_t* out8) {
+  int sign = 0;
+  size_t wc = 4;
+  uint64_t words[4] = {0, 0, 0, 0};
+  if (napi_get_value_bigint_words(env, v, &sign, &wc, words) != napi_ok) return false;
+  if (sign || wc > 4) return false;
+  for (int i = 0; i < 4; i++) {
+    out8[7 - 2 * i] = (uint32_t)words[i];
+    out8[6 - 2 * i] = (uint32_t)(words[i] >> 32);
+  }
+  return true;
+}
+
+napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  bool ap = false, as = false;
+  if (argc < 2 || napi_is_array(env, argv[0], &ap) != napi_ok || !ap || napi_is_array(env, argv[1], &as) != napi_ok ||
+      !as) {
+    napi_throw_type_error(env, nullptr, "computeMsmBigInt(points: BigIntPoint[], scalars: bigint[], windowSize?)");
+    return nullptr;
+  }
+  uint32_t np_ = 0, ns = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &np_));
+  NAPI_OK(napi_get_array_length(env, argv[1], &ns));
+  Job* j = new Job();
+  j->n = std::min(np_, ns);
+  j->points.resize(j->n * 32);
+  j->scalars.resize(j->n * 8);
+  static const char* keys[4] = {"x", "y", "t", "z"};
+  for (uint32_t i = 0; i < j->n; i++) {
+    napi_value p, s;
+    if (napi_get_element(env, argv[0], i, &p) != napi_ok || napi_get_element(env, argv[1], i, &s) != napi_ok) {
+      delete j;
+      napi_throw_error(env, nullptr, "bad input element");
+      return nullptr;
+    }
+    for (int k = 0; k < 4; k++) {
+      napi_value c;
+      if (napi_get_named_property(env, p, keys[k], &c) != napi_ok || !bigint_be(env, c, &j->points[i * 32 + 8 * k])) {
+        delete j;
+        napi_throw_range_error(env, nullptr, "point coordinate must be a bigint in [0, 2^256)");
+        return nullptr;
+      }
+    }
+    if (!bigint_be(env, s, &j->scalars[i * 8])) {
+      delete j;
+      napi_throw_range_error(env, nullptr, "scalar must be a bigint in [0, 2^256)");
+      return nullptr;
+    }
+  }
+  j->window = argc > 2 ? get_window(env, argv[2]) : 0;
+  return start_job(env, j);
+}
+
+napi_value make_u32(napi_env env, const uint32_t* src, size_t n) {
+  napi_value ab, arr;
+  void* buf;
+  NAPI_OK(napi_create_arraybuffer(env, n * 4, &buf, &ab));
+  if (n) memcpy(buf, src, n * 4);
+  NAPI_OK(napi_create_typedarray(env, napi_uint32_array, n, ab, 0, &arr));
+  return arr;
+}
+
+napi_value throw_rc(napi_env env, int rc) {
+  std::string m = std::string("libmsm: ") + msm_strerror(rc);
+  napi_throw_error(env, std::to_string(rc).c_str(), m.c_str());
+  return nullptr;
+}
+
+napi_value PointAddAffine(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint32_t *a, *b;
+  size_t la, lb;
+  if (argc < 2 || !get_u32_array(env, argv[0], &a, &la) || !get_u32_array(env, argv[1], &b, &lb) || la != 16 ||
+      lb != 16) {
+    napi_throw_type_error(env, nullptr, "pointAddAffine(a: Uint32Array(16), b: Uint32Array(16))");
+    return nullptr;
+  }
+  uint32_t out[16];
+  int rc = msm_point_add_affine(a, b, out);
+  if (rc != MSM_OK) return throw_rc(env, rc);
+  return make_u32(env, out, 16);
+}
+
+napi_value Split(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint32_t* sc;
+  size_t len;
+  uint32_t c = argc > 0 ? get_window(env, argv[0]) : 0;
+  if (argc < 2 || !get_u32_array(env, argv[1], &sc, &len)) {
+    napi_throw_type_error(env, nullptr, "split(windowSize, scalars: Uint32Array)");
+    return nullptr;
+  }
+  size_t n = len / 8;
+  uint32_t nw = msm_split_windows(c);
+  std::vector<uint32_t> out((size_t)nw * n + 1);
+  int rc = msm_split(c, sc, n, out.data());
+  if (rc != MSM_OK) return throw_rc(env, rc);
+  return make_u32(env, out.data(), (size_t)nw * n);
+}
+
+napi_value BestWindowSize(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  double n = 0;
+  if (argc > 0) napi_get_value_double(env, argv[0], &n);
+  napi_value r;
+  NAPI_OK(napi_create_uint32(env, msm_best_window((size_t)n), &r));
+  return r;
+}
+
+napi_value Init(napi_env env, napi_callback_info) {
+  napi_value r;
+  NAPI_OK(napi_create_int32(env, msm_init(), &r));
+  return r;
+}
+
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+  napi_value r;
+  NAPI_OK(napi_create_int32(env, msm_device_count(), &r));
+  return r;
+}
+
+napi_value StrError(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t code = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &code);
+  napi_value r;
+  NAPI_OK(napi_create_string_utf8(env, msm_strerror(code), NAPI_AUTO_LENGTH, &r));
+  return r;
+}
+
+napi_value ModuleInit(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"computeMsmU32", nullptr, ComputeMsmU32, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"computeMsmBigInt", nullptr, ComputeMsmBigInt, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"pointAddAffine", nullptr, PointAddAffine, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"split", nullptr, Split, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"bestWindowSize", nullptr, BestWindowSize, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"init", nullptr, Init, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"strerror", nullptr, StrError, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, ModuleInit)

@@ -1,0 +1,19 @@
+// Type surface of submission.mjs — identical to the reference's (src/reference/types.ts:1-13,
+// src/submission/submission.ts:25-28).
+export type BigIntPoint = { x: bigint; y: bigint; t: bigint; z: bigint };
+export type U32ArrayPoint = { x: Uint32Array; y: Uint32Array; t: Uint32Array; z: Uint32Array };
+
+export declare const compute_msm: (
+  baseAffinePoints: BigIntPoint[] | U32ArrayPoint[],
+  scalars: bigint[] | Uint32Array[],
+  options?: { windowSize?: number }
+) => Promise<{ x: bigint; y: bigint }>;
+
+export declare function getBestWindowSize(n: number): number;
+export declare function u32ArrayToBigInts(u32Array: Uint32Array): bigint[];
+export declare const split_dynamic: (windowSize: number, scalars: Uint32Array) => Uint32Array;
+export declare const point_add_affine: (a: Uint32Array, b: Uint32Array) => Uint32Array;
+export declare const init: () => number;
+export declare const deviceCount: () => number;
+export declare const nUint32PerScalar: 8;
+export declare const nUint32PerPoint: 32;

@@ -1,0 +1,89 @@
+// compute_msm — drop-in for the reference's public entry point
+// (src/submission/submission.ts:25-157), routed through the N-API addon (addon.cc) into
+// libmsm's HIP kernels on MI355X.  Same signature and result:
+//
+//   compute_msm(baseAffinePoints: BigIntPoint[] | U32ArrayPoint[],
+//               scalars: bigint[] | Uint32Array[]) => Promise<{ x: bigint, y: bigint }>
+//
+// The browser-only knobs (?windowSize=, submission.ts:29-33) become an optional third
+// argument { windowSize } or the MSM_WINDOW_SIZE environment variable.
+// There is no WebGPU/WGSL/CPU fallback: without the addon or a gfx950 device this rejects.
+import { createRequire } from "module";
+
+const require = createRequire(import.meta.url);
+const addon = require("./msm_napi.node");
+
+export const nUint32PerScalar = 8; // consts.ts:1
+export const nUint32PerPoint = 4 * nUint32PerScalar; // consts.ts:3
+
+// getBestWindowSize (submission.ts:18-23), tuned for libmsm's signed-digit pipeline.
+export function getBestWindowSize(n) {
+  return addon.bestWindowSize(n);
+}
+
+function windowFrom(options) {
+  if (options && options.windowSize) return options.windowSize | 0;
+  const env = typeof process !== "undefined" && process.env ? process.env.MSM_WINDOW_SIZE : undefined;
+  return env ? parseInt(env, 10) : 0;
+}
+
+// u32ArrayToBigInts (submission.ts:159-175): 8 big-endian words per value.
+export function u32ArrayToBigInts(u32Array) {
+  const out = [];
+  for (let i = 0; i < u32Array.length; i += 8) {
+    let v = 0n;
+    for (let j = 0; j < 8 && i + j < u32Array.length; j++) v = (v << 32n) | BigInt(u32Array[i + j]);
+    out.push(v);
+  }
+  return out;
+}
+
+// U32ArrayPoint[] / Uint32Array[] -> flat wire buffers (submission.ts:75-86 layout x|y|t|z).
+function flattenU32(points, scalars) {
+  const n = Math.min(points.length, scalars.length);
+  const pointBuffer = new Uint32Array(n * nUint32PerPoint);
+  const scalarBuffer = new Uint32Array(n * nUint32PerScalar);
+  for (let i = 0; i < n; i++) {
+    const p = points[i];
+    pointBuffer.set(p.x, i * 32);
+    pointBuffer.set(p.y, i * 32 + 8);
+    pointBuffer.set(p.t, i * 32 + 16);
+    pointBuffer.set(p.z, i * 32 + 24);
+    scalarBuffer.set(scalars[i], i * 8);
+  }
+  return [pointBuffer, scalarBuffer];
+}
+
+export const compute_msm = async (baseAffinePoints, scalars, options) => {
+  const windowSize = windowFrom(options);
+  const hasBigInt =
+    (baseAffinePoints.length > 0 && typeof baseAffinePoints[0].x === "bigint") ||
+    (scalars.length > 0 && typeof scalars[0] === "bigint");
+  let result;
+  if (hasBigInt) {
+    // native marshalling (napi_get_value_bigint_words) replaces convert_worker.ts
+    const pts = typeof baseAffinePoints[0].x === "bigint" ? baseAffinePoints : baseAffinePoints.map(toBigIntPoint);
+    const sc = typeof scalars[0] === "bigint" ? scalars : scalars.map((s) => u32ArrayToBigInts(s)[0]);
+    result = await addon.computeMsmBigInt(pts, sc, windowSize);
+  } else {
+    const [pointBuffer, scalarBuffer] = flattenU32(baseAffinePoints, scalars);
+    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize);
+  }
+  const [x, y] = u32ArrayToBigInts(result);
+  return { x, y };
+};
+
+function toBigIntPoint(p) {
+  return {
+    x: u32ArrayToBigInts(p.x)[0],
+    y: u32ArrayToBigInts(p.y)[0],
+    t: u32ArrayToBigInts(p.t)[0],
+    z: u32ArrayToBigInts(p.z)[0],
+  };
+}
+
+// Reference helper entry points (lib.rs:196-253), exposed for parity with the wasm module.
+export const split_dynamic = (windowSize, scalarsU32) => addon.split(windowSize, scalarsU32);
+export const point_add_affine = (a16, b16) => addon.pointAddAffine(a16, b16);
+export const init = () => addon.init();
+export const deviceCount = () => addon.deviceCount();

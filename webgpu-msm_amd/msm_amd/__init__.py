@@ -1,0 +1,350 @@
+"""msm_amd — Python host binding of libmsm (MI355X Edwards-BLS12 MSM).
+
+Mirrors the reference's public surface (src/submission/submission.ts:25-157):
+
+    compute_msm(base_affine_points, scalars, window_size=None) -> (x, y)
+
+with the same input shapes (BigIntPoint-like dicts / tuples, or U32ArrayPoint-like wire words),
+the same output ({x, y} as ints, identity = (0, 1)), and the reference's helper entry points
+(split_dynamic, point_add_affine, get_best_window_size).  All compute runs in libmsm's HIP
+kernels; there is no CPU fallback: if the shared library or a gfx950 device is missing, calls
+raise MsmError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+__all__ = [
+    "MsmError", "MsmOpts", "load", "compute_msm", "compute_msm_wire", "compute_msm_device",
+    "compute_msm_partial", "compute_msm_device_partial", "combine_partials", "point_add_affine",
+    "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count",
+    "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
+]
+
+P = 8444461749428370424248824938781546531375899335154063827935233455917409239041
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "_lib", "libmsm.so")
+
+
+class MsmError(RuntimeError):
+    def __init__(self, code: int, where: str = ""):
+        self.code = code
+        msg = _strerror(code)
+        super().__init__(f"libmsm error {code} ({msg}){' in ' + where if where else ''}")
+
+
+class MsmOpts(ctypes.Structure):
+    _fields_ = [("window_bits", ctypes.c_uint32), ("run_length", ctypes.c_uint32),
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class MsmProfile(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in (
+        "prepare_points", "recode_count", "coarse_scan", "coarse_scatter", "fine_sort", "accumulate",
+        "fixup", "bucket_reduce_1", "bucket_reduce_2", "readback", "device_total", "host_tail")] + [
+        ("entries", ctypes.c_uint64), ("window_bits", ctypes.c_uint32), ("windows", ctypes.c_uint32),
+        ("run_length", ctypes.c_uint32), ("chunk_len", ctypes.c_uint32)]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib_path() -> str:
+    return _LIB
+
+
+def load() -> ctypes.CDLL:
+    """Load libmsm.so (built in-tree by `make -C webgpu-msm_amd`).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB):
+        raise MsmError(-6, f"libmsm.so not built at {_LIB} (run __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7) that
+    # its libraries NEED by the unversioned name.  Loading torch first lets libmsm bind to that
+    # same runtime by soname; loading libmsm first would pull /opt/rocm's copy and torch would
+    # then initialise a second runtime that sees no devices.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(_LIB)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    optp = ctypes.POINTER(MsmOpts)
+    sig = {
+        "msm_init": ([], ctypes.c_int),
+        "msm_shutdown": ([], None),
+        "msm_device_count": ([], ctypes.c_int),
+        "msm_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "msm_best_window": ([sz], ctypes.c_uint32),
+        "msm_compute": ([vp, vp, sz, optp, u32p], ctypes.c_int),
+        "msm_compute_partial": ([vp, vp, sz, optp, u32p], ctypes.c_int),
+        "msm_compute_device": ([vp, vp, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_compute_device_partial": ([vp, vp, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_compute_batch_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_combine_partials": ([vp, sz, u32p], ctypes.c_int),
+        "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
+        "msm_split": ([ctypes.c_uint32, vp, sz, u32p], ctypes.c_int),
+        "msm_split_windows": ([ctypes.c_uint32], ctypes.c_uint32),
+        "msm_set_profiling": ([ctypes.c_int], ctypes.c_int),
+        "msm_gen_points": ([u32p, ctypes.c_uint64, ctypes.c_uint64, sz, u32p], ctypes.c_int),
+        "msm_gen_scalars": ([ctypes.c_uint64, sz, u32p], ctypes.c_int),
+        "msm_last_profile": ([ctypes.POINTER(MsmProfile)], ctypes.c_int),
+        "msm_test_field_op": ([ctypes.c_uint32, vp, vp, u32p, sz], ctypes.c_int),
+        "msm_test_point_op": ([ctypes.c_uint32, vp, vp, u32p, sz], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _strerror(code: int) -> str:
+    try:
+        return load().msm_strerror(code).decode()
+    except Exception:  # library itself missing
+        return "libmsm unavailable"
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != 0:
+        raise MsmError(rc, where)
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p) if a.size else None
+
+
+def _out(n: int) -> Tuple[np.ndarray, ctypes.POINTER(ctypes.c_uint32)]:
+    o = np.zeros(n, dtype=np.uint32)
+    return o, o.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1):
+    return ctypes.byref(MsmOpts(int(window_size or 0), int(run_length or 0), int(device), 0))
+
+
+def wire_to_int(words: Iterable[int]) -> int:
+    v = 0
+    for w in words:
+        v = (v << 32) | int(w)
+    return v
+
+
+def _int_be_words(v: int) -> bytes:
+    if v < 0 or v >= 1 << 256:
+        raise ValueError("value does not fit 256 bits")
+    return int(v).to_bytes(32, "big")
+
+
+def points_to_wire(points) -> np.ndarray:
+    """BigIntPoint[] ({x,y,t,z} ints or (x,y,t,z) tuples) or U32ArrayPoint[] -> wire [n, 32] u32.
+
+    Same layout as submission.ts:35-86 / convert_worker.ts:8-57: x|y|t|z, each 8 BE words.
+    A numpy array of shape [n, 32] is taken as already-marshalled wire data.
+    """
+    if isinstance(points, np.ndarray):
+        return _u32(points).reshape(-1, 32)
+    pts = list(points)
+    if not pts:
+        return np.zeros((0, 32), dtype=np.uint32)
+    first = pts[0]
+    keys = ("x", "y", "t", "z")
+    if isinstance(first, dict):
+        get = lambda p, k: p[k]  # noqa: E731
+    elif hasattr(first, "x"):
+        get = lambda p, k: getattr(p, k)  # noqa: E731
+    else:
+        get = lambda p, k: p[keys.index(k)]  # noqa: E731
+    sample = get(first, "x")
+    if isinstance(sample, (int, np.integer)):
+        buf = b"".join(_int_be_words(int(get(p, k))) for p in pts for k in keys)
+        return np.frombuffer(buf, dtype=">u4").astype(np.uint32).reshape(-1, 32)
+    out = np.empty((len(pts), 32), dtype=np.uint32)
+    for i, p in enumerate(pts):  # U32ArrayPoint: four BE u32[8]
+        for j, k in enumerate(keys):
+            out[i, 8 * j: 8 * j + 8] = np.asarray(get(p, k), dtype=np.uint32)
+    return out
+
+
+def scalars_to_wire(scalars) -> np.ndarray:
+    """bigint[] or Uint32Array[] (BE u32[8]) -> [n, 8] u32."""
+    if isinstance(scalars, np.ndarray):
+        return _u32(scalars).reshape(-1, 8)
+    sc = list(scalars)
+    if not sc:
+        return np.zeros((0, 8), dtype=np.uint32)
+    if isinstance(sc[0], (int, np.integer)):
+        buf = b"".join(_int_be_words(int(s)) for s in sc)
+        return np.frombuffer(buf, dtype=">u4").astype(np.uint32).reshape(-1, 8)
+    return np.stack([np.asarray(s, dtype=np.uint32).reshape(8) for s in sc])
+
+
+def _xy(o: np.ndarray) -> Tuple[int, int]:
+    return wire_to_int(o[:8]), wire_to_int(o[8:16])
+
+
+def get_best_window_size(n: int) -> int:
+    """getBestWindowSize (submission.ts:18-23), retuned for the signed-digit GPU pipeline."""
+    return int(load().msm_best_window(n))
+
+
+def compute_msm_wire(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
+                     run_length: Optional[int] = None, device: int = -1) -> Tuple[int, int]:
+    L = load()
+    pts = _u32(points_wire).reshape(-1, 32)
+    sc = _u32(scalars_wire).reshape(-1, 8)
+    n = min(pts.shape[0], sc.shape[0])  # the oracle zips to the shorter length
+    pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
+    o, op = _out(16)
+    _check(L.msm_compute(_ptr(pts), _ptr(sc), n, _opts(window_size, run_length, device), op), "msm_compute")
+    return _xy(o)
+
+
+def compute_msm(base_affine_points, scalars, window_size: Optional[int] = None,
+                run_length: Optional[int] = None, device: int = -1) -> Tuple[int, int]:
+    """compute_msm (submission.ts:25-157): MSM of BigIntPoint[]/U32ArrayPoint[] with bigint[]/Uint32Array[]."""
+    return compute_msm_wire(points_to_wire(base_affine_points), scalars_to_wire(scalars), window_size,
+                            run_length, device)
+
+
+def compute_msm_partial(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
+                        device: int = -1) -> np.ndarray:
+    L = load()
+    pts = _u32(points_wire).reshape(-1, 32)
+    sc = _u32(scalars_wire).reshape(-1, 8)
+    n = min(pts.shape[0], sc.shape[0])
+    pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
+    o, op = _out(32)
+    _check(L.msm_compute_partial(_ptr(pts), _ptr(sc), n, _opts(window_size, None, device), op), "msm_compute_partial")
+    return o
+
+
+def _dev_ptr(t) -> int:
+    return int(t.data_ptr()) if hasattr(t, "data_ptr") else int(t)
+
+
+def compute_msm_device(d_points, d_scalars, n: int, window_size: Optional[int] = None,
+                       run_length: Optional[int] = None, device: int = -1, stream: int = 0) -> Tuple[int, int]:
+    """Inputs already in HBM (torch tensors or raw device pointers, wire layout)."""
+    L = load()
+    o, op = _out(16)
+    _check(L.msm_compute_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, run_length, device),
+                                stream or None, op), "msm_compute_device")
+    return _xy(o)
+
+
+def compute_msm_device_partial(d_points, d_scalars, n: int, window_size: Optional[int] = None,
+                               device: int = -1, stream: int = 0) -> np.ndarray:
+    L = load()
+    o, op = _out(32)
+    _check(L.msm_compute_device_partial(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, None, device),
+                                        stream or None, op), "msm_compute_device_partial")
+    return o
+
+
+def compute_msm_batch_device(d_points, d_scalars, n: int, count: int, window_size: Optional[int] = None,
+                             device: int = -1, stream: int = 0) -> np.ndarray:
+    L = load()
+    o, op = _out(16 * count)
+    _check(L.msm_compute_batch_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n, count,
+                                      _opts(window_size, None, device), stream or None, op), "msm_compute_batch_device")
+    return o.reshape(count, 16)
+
+
+def combine_partials(partials: np.ndarray) -> Tuple[int, int]:
+    L = load()
+    p = _u32(partials).reshape(-1, 32)
+    o, op = _out(16)
+    _check(L.msm_combine_partials(_ptr(p), p.shape[0], op), "msm_combine_partials")
+    return _xy(o)
+
+
+def point_add_affine(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:
+    """point_add_affine (lib.rs:240-253)."""
+    L = load()
+    aw = np.frombuffer(_int_be_words(a[0]) + _int_be_words(a[1]), dtype=">u4").astype(np.uint32)
+    bw = np.frombuffer(_int_be_words(b[0]) + _int_be_words(b[1]), dtype=">u4").astype(np.uint32)
+    o, op = _out(16)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    _check(L.msm_point_add_affine(aw.ctypes.data_as(u32p), bw.ctypes.data_as(u32p), op), "msm_point_add_affine")
+    return _xy(o)
+
+
+def split_dynamic(window_size: int, scalars_wire: np.ndarray) -> np.ndarray:
+    """split_dynamic (lib.rs:196-202): [n_windows * n] u32, window 0 most significant."""
+    L = load()
+    sc = _u32(scalars_wire).reshape(-1, 8)
+    nw = L.msm_split_windows(window_size)
+    o, op = _out(max(nw * sc.shape[0], 1))
+    _check(L.msm_split(window_size, _ptr(sc), sc.shape[0], op), "msm_split")
+    return o[: nw * sc.shape[0]]
+
+
+BENCH_G = (2796670805570508460920584878396618987767121022598342527208237783066948667246,
+           8134280397689638111748378379571739274369602049665521098046934931245960532166)
+XORSHIFT_SEED = 0x9E3779B97F4A7C15
+
+
+def gen_points(n: int, k0: int = 1, step: int = 1, base: Tuple[int, int] = BENCH_G) -> np.ndarray:
+    """Wire points [n, 32]: (k0 + i*step) * base (the benchmark page's fixed base, AllBenchmarks.tsx:111-119)."""
+    L = load()
+    g = np.frombuffer(_int_be_words(base[0]) + _int_be_words(base[1]), dtype=">u4").astype(np.uint32)
+    o, op = _out(max(n, 1) * 32)
+    _check(L.msm_gen_points(g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), k0, step, n, op), "msm_gen_points")
+    return o[: n * 32].reshape(n, 32)
+
+
+def gen_scalars(n: int, seed: int = XORSHIFT_SEED) -> np.ndarray:
+    """Scalars [n, 8] BE: xorshift64(13,7,17), 4 words each (first most significant), mod p."""
+    L = load()
+    o, op = _out(max(n, 1) * 8)
+    _check(L.msm_gen_scalars(seed, n, op), "msm_gen_scalars")
+    return o[: n * 8].reshape(n, 8)
+
+
+def set_profiling(enable: bool = True) -> None:
+    _check(load().msm_set_profiling(1 if enable else 0), "msm_set_profiling")
+
+
+def last_profile() -> dict:
+    prof = MsmProfile()
+    _check(load().msm_last_profile(ctypes.byref(prof)), "msm_last_profile")
+    return {name: getattr(prof, name) for name, _ in MsmProfile._fields_}
+
+
+def device_count() -> int:
+    return int(load().msm_device_count())
+
+
+def _test_field_op(op: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Device field op on canonical little-endian word arrays [n, 8] (test hook)."""
+    L = load()
+    a = _u32(a).reshape(-1, 8)
+    b = _u32(b).reshape(-1, 8)
+    o, op_ = _out(a.size)
+    _check(L.msm_test_field_op(op, _ptr(a), _ptr(b), op_, a.shape[0]), "msm_test_field_op")
+    return o.reshape(-1, 8)
+
+
+def _test_point_op(op: int, p: np.ndarray, q: np.ndarray) -> np.ndarray:
+    """Device point op on affine LE word arrays [n, 16] -> projective std LE words [n, 32] (test hook)."""
+    L = load()
+    p = _u32(p).reshape(-1, 16)
+    q = _u32(q).reshape(-1, 16)
+    o, op_ = _out(p.shape[0] * 32)
+    _check(L.msm_test_point_op(op, _ptr(p), _ptr(q), op_, p.shape[0]), "msm_test_point_op")
+    return o.reshape(-1, 32)
