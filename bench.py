@@ -102,9 +102,10 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
+    from msm_amd.dist import shard_range, sharded_msm_device
+
     n = args.n
-    lo = n * rank // world
-    hi = n * (rank + 1) // world
+    lo, hi = shard_range(n, rank, world)
     m = hi - lo
     pts = M.gen_points(m, k0=lo + 1)
     # scalars follow the global xorshift stream: generate all and slice (cheap, deterministic)
@@ -119,14 +120,7 @@ def main():
     def step():
         if world == 1:
             return M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
-        part = M.compute_msm_device_partial(d_pts, d_sc, m, window_size=window)
-        t = torch.from_numpy(part.view(np.int32)).to(dev)
-        gathered = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(gathered, t)
-        if rank == 0:
-            parts = np.stack([g.cpu().numpy().view(np.uint32) for g in gathered])
-            return M.combine_partials(parts)
-        return None
+        return sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
 
     for _ in range(args.warmup):
         res = step()

@@ -1,0 +1,116 @@
+"""C-ABI boundary checks that need no GPU: every symbol include/msm.h declares is exported by
+libmsm.so, and the host-side entry points (split, point_add_affine, combine, generators) agree
+with the oracle."""
+import ctypes
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import msm_amd as M
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "msm.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(msm_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("msm_init", "msm_compute", "msm_compute_device", "msm_point_add_affine", "msm_split",
+                 "msm_best_window", "msm_combine_partials", "msm_compute_batch_device"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", M.lib_path()], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+    L = M.load()
+    for n in declared_functions():
+        assert isinstance(getattr(L, n), ctypes._CFuncPtr)
+
+
+def test_addon_exports():
+    addon = os.path.join(ROOT, "webgpu-msm_amd", "js", "msm_napi.node")
+    assert os.path.exists(addon)
+    out = subprocess.run(["nm", "-D", addon], capture_output=True, text=True, check=True).stdout
+    assert "napi_module_register" in out  # NAPI_MODULE registers through a static constructor
+    node = shutil.which("node")
+    if node:
+        script = f"const a = require({addon!r}); console.log(Object.keys(a).sort().join(','))"
+        keys = subprocess.run([node, "-e", script], capture_output=True, text=True, check=True).stdout.strip()
+        assert keys.split(",") == sorted(["computeMsmU32", "computeMsmBigInt", "pointAddAffine", "split",
+                                          "bestWindowSize", "init", "deviceCount", "strerror"])
+
+
+def test_init_reports_device_state():
+    rc = M.load().msm_init()
+    assert rc in (0, -6)
+    if rc == -6:  # no GPU here: every compute entry must fail loudly (no CPU fallback)
+        with pytest.raises(M.MsmError) as e:
+            M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]))
+        assert e.value.code == -6
+
+
+def test_strerror_and_best_window():
+    assert M.load().msm_strerror(0) == b"ok"
+    assert M.load().msm_strerror(-3) == b"coordinate not in [0, p)"
+    for n in (1, 1 << 10, 1 << 16, 1 << 20, 1 << 24):
+        c = M.get_best_window_size(n)
+        assert 8 <= c <= 16
+    assert M.get_best_window_size(1 << 20) >= M.get_best_window_size(1 << 12)
+
+
+@pytest.mark.parametrize("c", [8, 9, 10, 11, 12, 13, 14, 15, 16, 20])
+def test_split_dynamic_matches_oracle(c):
+    rng = np.random.default_rng(c)
+    sc = rng.integers(0, 2**32, size=(37, 8), dtype=np.uint64).astype(np.uint32)
+    sc[0] = 0xFFFFFFFF
+    sc[1] = 0
+    assert np.array_equal(M.split_dynamic(c, sc), O.split(c, sc))
+
+
+def test_split_rejects_bad_window():
+    with pytest.raises(M.MsmError):
+        M.split_dynamic(0, np.zeros((1, 8), np.uint32))
+
+
+def test_point_add_affine_matches_oracle(golden):
+    for a, b, exp in golden["kats"]["add_points_x"]["cases"]:
+        pa, pb = O.point_from_x(int(a)), O.point_from_x(int(b))
+        got = M.point_add_affine(pa, pb)
+        assert got == O.aff_add(pa, pb)
+        assert got[0] == int(exp)
+    assert M.point_add_affine(O.G, O.IDENTITY) == O.G
+    assert M.point_add_affine(O.G, O.aff_neg(O.G)) == O.IDENTITY
+    with pytest.raises(M.MsmError):
+        M.point_add_affine((O.P, 1), O.G)
+
+
+def test_combine_partials():
+    pts = [O.scalar_mul(O.G, k) for k in (3, 10, 77, 1000)]
+    parts = np.zeros((4, 32), np.uint32)
+    for i, (x, y) in enumerate(pts):
+        z = 5 + i  # projective, z != 1
+        X, Y, T = x * z % O.P, y * z % O.P, x * y % O.P * z % O.P
+        for j, v in enumerate((X, Y, T, z)):
+            parts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
+    assert M.combine_partials(parts) == O.scalar_mul(O.G, 3 + 10 + 77 + 1000)
+    assert M.combine_partials(np.zeros((0, 32), np.uint32)) == O.IDENTITY
+
+
+def test_generators_match_oracle():
+    assert np.array_equal(M.gen_points(300, k0=5, step=9), O.gen_points(300, k0=5, step=9))
+    assert np.array_equal(M.gen_points(5000), O.gen_points(5000))
+    assert np.array_equal(M.gen_scalars(777, seed=3), O.xorshift_scalars_np(777, seed=3))

@@ -1,0 +1,63 @@
+"""World-size-2 gloo rehearsal of the point-sharded path (msm_amd/dist.py) on CPU.
+
+Each rank's shard MSM is computed by the oracle here (no GPU in this container) and shipped in
+the same 32-word projective partial format libmsm's msm_compute_device_partial produces; the
+gather / join code under test is the one bench.py runs over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "webgpu-msm_amd")]
+    import torch.distributed as dist
+    from msm_amd.dist import shard_range, gather_partials, combine_on_root
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(n, rank, world)
+    ss = O.xorshift_scalars(n)[lo:hi]
+    x, y = O.closed_form_msm(range(lo + 1, hi + 1), ss) if hi > lo else O.IDENTITY
+    z = 3 + rank  # ship a non-normalised projective partial, as the GPU path does
+    part = np.zeros(32, np.uint32)
+    for j, v in enumerate((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)):
+        part[8 * j: 8 * j + 8] = O.int_to_be_words(v)
+    parts = gather_partials(part)
+    res = combine_on_root(parts, rank)
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1000), (2, 1), (3, 4096)])
+def test_sharded_join_gloo(world, n):
+    from oracle import oracle as O
+    from msm_amd.dist import shard_range
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == O.closed_form_msm(range(1, n + 1), O.xorshift_scalars(n))
+    assert sum(b - a for a, b in (shard_range(n, r, world) for r in range(world))) == n

@@ -1,0 +1,90 @@
+"""Host-side marshalling and the TypeScript/JS surface (node), CPU only."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import msm_amd as M
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JS = os.path.join(ROOT, "webgpu-msm_amd", "js", "submission.mjs")
+NODE = shutil.which("node")
+
+
+def test_points_to_wire_forms_agree(golden):
+    pts = O.gen_points(20, k0=4)
+    as_int = [{k: O.be_words_to_int(pts[i, 8 * j: 8 * j + 8]) for j, k in enumerate("xytz")} for i in range(20)]
+    as_tuple = [tuple(p[k] for k in "xytz") for p in as_int]
+    as_u32 = [{k: pts[i, 8 * j: 8 * j + 8].copy() for j, k in enumerate("xytz")} for i in range(20)]
+    for form in (as_int, as_tuple, as_u32, pts):
+        assert np.array_equal(M.points_to_wire(form), pts)
+    assert M.points_to_wire([]).shape == (0, 32)
+
+
+def test_scalars_to_wire_limb_order(golden):
+    cases = golden["kats"]["be_limbs"]["cases"]
+    vals = [int(v) for v, _ in cases]
+    w = M.scalars_to_wire(vals)
+    assert w.tolist() == [words for _, words in cases]
+    assert np.array_equal(M.scalars_to_wire([np.array(x, np.uint32) for _, x in cases]), w)
+    with pytest.raises(ValueError):
+        M.scalars_to_wire([1 << 256])
+    assert M.wire_to_int(w[4]) == O.P
+
+
+def _node(script):
+    out = subprocess.run([NODE, "--input-type=module", "-e", script], capture_output=True, text=True, timeout=120,
+                         cwd=os.path.dirname(JS))
+    assert out.returncode == 0, out.stderr
+    return out.stdout
+
+
+@pytest.mark.skipif(NODE is None, reason="node not installed")
+def test_js_surface_helpers(golden):
+    cases = golden["kats"]["be_limbs"]["cases"]
+    script = f"""
+import * as m from {json.dumps(JS)};
+const cases = {json.dumps(cases)};
+const res = {{}};
+res.limbs = cases.map(([v, w]) => m.u32ArrayToBigInts(new Uint32Array(w))[0].toString() === v);
+res.best = [1<<16, 1<<20].map((n) => m.getBestWindowSize(n));
+const sc = new Uint32Array([0x12345678, 0x9abcdef0, 1, 2, 3, 4, 5, 0xffffffff]);
+res.split = Array.from(m.split_dynamic(13, sc));
+console.log(JSON.stringify(res));
+"""
+    res = json.loads(_node(script))
+    assert all(res["limbs"])
+    assert res["best"] == [M.get_best_window_size(1 << 16), M.get_best_window_size(1 << 20)]
+    sc = np.array([0x12345678, 0x9ABCDEF0, 1, 2, 3, 4, 5, 0xFFFFFFFF], np.uint32)
+    assert res["split"] == O.split(13, sc).tolist()
+
+
+@pytest.mark.skipif(NODE is None, reason="node not installed")
+def test_js_point_add_affine(golden):
+    a, b, exp = golden["kats"]["add_points_x"]["cases"][0]
+    pa, pb = O.point_from_x(int(a)), O.point_from_x(int(b))
+    wa = O.int_to_be_words(pa[0]) + O.int_to_be_words(pa[1])
+    wb = O.int_to_be_words(pb[0]) + O.int_to_be_words(pb[1])
+    script = f"""
+import * as m from {json.dumps(JS)};
+const r = m.point_add_affine(new Uint32Array({wa}), new Uint32Array({wb}));
+console.log(m.u32ArrayToBigInts(r).map(String).join(","));
+"""
+    x, y = _node(script).strip().split(",")
+    assert int(x) == int(exp) and (int(x), int(y)) == O.aff_add(pa, pb)
+
+
+@pytest.mark.skipif(NODE is None, reason="node not installed")
+def test_js_compute_msm_fails_loudly_without_device():
+    if M.load().msm_init() == 0:
+        pytest.skip("a GPU is present; covered by tests/test_gpu_js.py")
+    script = f"""
+import * as m from {json.dumps(JS)};
+m.compute_msm([{{x: 1n, y: 2n, t: 2n, z: 1n}}], [3n]).then(
+  () => console.log("resolved"), (e) => console.log("rejected " + e.code));
+"""
+    assert _node(script).strip() == "rejected -6"

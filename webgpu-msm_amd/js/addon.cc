@@ -261,14 +261,14 @@ napi_value StrError(napi_env env, napi_callback_info info) {
 
 napi_value ModuleInit(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
-      {"computeMsmU32", nullptr, ComputeMsmU32, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"computeMsmBigInt", nullptr, ComputeMsmBigInt, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"pointAddAffine", nullptr, PointAddAffine, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"split", nullptr, Split, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"bestWindowSize", nullptr, BestWindowSize, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"init", nullptr, Init, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
-      {"strerror", nullptr, StrError, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"computeMsmU32", nullptr, ComputeMsmU32, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"computeMsmBigInt", nullptr, ComputeMsmBigInt, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"pointAddAffine", nullptr, PointAddAffine, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"split", nullptr, Split, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"bestWindowSize", nullptr, BestWindowSize, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"init", nullptr, Init, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"strerror", nullptr, StrError, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -1,0 +1,52 @@
+"""Point-sharded multi-GPU MSM: one process per GPU, partial points joined over RCCL/xGMI.
+
+MSM is linear in the (point, scalar) vector, so every rank computes the MSM of a contiguous
+1/world slice of the inputs on its own GPU (no data-path collective) and the per-rank partial
+points (projective X|Y|T|Z, 128 B each) are all-gathered and added on rank 0 — the
+generalisation of the reference's CPU/GPU co-compute split and its single affine join
+(src/submission/submission.ts:116-154, msm-wasm/src/lib.rs:240-253).  The join is an elliptic
+curve addition, not an RCCL reduction op, hence all_gather + host add.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) slice of n points owned by `rank` (sizes differ by at most 1)."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.ndarray:
+    """all_gather one 32-word partial per rank; returns [world, 32] u32 on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    t = torch.from_numpy(np.ascontiguousarray(partial_xyzt_be, dtype=np.uint32).view(np.int32).copy())
+    if device is not None:
+        t = t.to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    return np.stack([o.cpu().numpy().view(np.uint32) for o in out])
+
+
+def combine_on_root(parts: np.ndarray, rank: int, root: int = 0) -> Optional[Tuple[int, int]]:
+    """Rank `root` adds the gathered partials (libmsm host EC adds) into the affine result."""
+    if rank != root:
+        return None
+    from . import combine_partials
+
+    return combine_partials(parts)
+
+
+def sharded_msm_device(d_points, d_scalars, n_local: int, rank: int, device=None, window_size=None,
+                       group=None) -> Optional[Tuple[int, int]]:
+    """One sharded MSM step: local partial on this rank's GPU, gather, join on rank 0."""
+    from . import compute_msm_device_partial
+
+    part = compute_msm_device_partial(d_points, d_scalars, n_local, window_size=window_size)
+    parts = gather_partials(part, device=device, group=group)
+    return combine_on_root(parts, rank)
