@@ -17,7 +17,7 @@ NODE = shutil.which("node")
 
 @pytest.mark.skipif(NODE is None, reason="node not installed")
 @pytest.mark.parametrize("form", ["bigint", "u32"])
-def test_compute_msm_js(form):
+def test_compute_msm_js(form, tmp_path):
     n = 500
     pts = O.gen_points(n, k0=21, step=13)
     ss = O.xorshift_scalars(n, seed=77)
@@ -40,7 +40,9 @@ if ("{form}" === "bigint") {{
 m.compute_msm(points, scalars).then((r) => console.log(r.x.toString() + "," + r.y.toString()),
   (e) => {{ console.error(e); process.exit(3); }});
 """
-    out = subprocess.run([NODE, "--input-type=module", "-e", script], capture_output=True, text=True, timeout=300)
+    path = tmp_path / "run_js.mjs"
+    path.write_text(script)
+    out = subprocess.run([NODE, str(path)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     x, y = out.stdout.strip().split(",")
     assert (int(x), int(y)) == exp

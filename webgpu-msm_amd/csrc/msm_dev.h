@@ -14,8 +14,10 @@ struct MsmDims {
   uint32_t fb;     // fine bits sorted inside one coarse bin = min(c-1, 9)
   uint32_t nbc;    // coarse bins per window = B >> fb
   uint32_t nbins;  // W * nbc
-  uint32_t spt;    // scalars per thread in the recode / scatter kernels
+  uint32_t ch;     // digits per partition workgroup (one window chunk)
+  uint32_t nch;    // chunks per window = ceil(n / ch)
 };
+
 
 constexpr uint32_t PT_WORDS = 36;  // extended point, 4 x 9 limbs (144 B)
 constexpr uint32_t PRE_WORDS = 32;  // precomputed affine point record (108 B used, 128 B stride)

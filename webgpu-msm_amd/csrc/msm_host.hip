@@ -104,9 +104,9 @@ struct DevCtx {
   int device = -1;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  Buf wire_points, wire_scalars, pts, err, coarse_count, coarse_base, coarse_cursor;
+  Buf wire_points, wire_scalars, pts, err, digits, hist_rows, rel, colsum, bin_base;
   Buf part_entry, part_fine, sorted_entry, sorted_key, bucket_count, buckets;
-  Buf run_head, run_tail, head_key, tail_key, red_U, red_T, red_out;
+  Buf run_head, run_tail, head_key, tail_next, fix_list, red_U, red_T, red_out;
   HostBuf h_out;
   hipEvent_t ev[PH_COUNT] = {};
   bool profiling = false;
@@ -188,10 +188,16 @@ int make_plan(size_t n, const msm_opts* o, Plan* pl) {
   d.c = c;
   d.B = 1u << (c - 1);
   d.W = (257 + c - 1) / c;
-  d.fb = std::min<uint32_t>(c - 1, 9);
-  d.nbc = d.B >> d.fb;
+  // Coarse bins: aim at ~4K entries per bin (half the LDS staging capacity of k_fine_sort) with at
+  // most FS_MAXF buckets per bin.  Partition chunks hold >= 64 entries per bin slice.
+  uint32_t nbc = 1;
+  while (nbc < d.B && nbc < 256 && (size_t)nbc * 4096 < n) nbc <<= 1;
+  while (nbc < d.B && (d.B / nbc) > FS_MAXF) nbc <<= 1;
+  d.nbc = nbc;
+  d.fb = ilog2(d.B / nbc);
   d.nbins = d.W * d.nbc;
-  d.spt = 16;
+  d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
+  d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
   pl->d = d;
   pl->K = (o && o->run_length) ? o->run_length : 32;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
@@ -213,9 +219,11 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   if ((rc = c->buf.ensure(bytes)) != MSM_OK) return rc
   ENS(pts, (size_t)d.n * PRE_WORDS * 4);
   ENS(err, 16);
-  ENS(coarse_count, (size_t)d.nbins * 4);
-  ENS(coarse_base, ((size_t)d.nbins + 1) * 4);
-  ENS(coarse_cursor, (size_t)d.nbins * 4);
+  ENS(digits, (size_t)d.W * d.n * 4);
+  ENS(hist_rows, (size_t)d.nch * d.nbins * 4);
+  ENS(rel, (size_t)d.nch * d.nbins * 4);
+  ENS(colsum, (size_t)d.nbins * 4);
+  ENS(bin_base, ((size_t)d.nbins + 1) * 4);
   ENS(part_entry, pl.Mmax * 4);
   ENS(part_fine, pl.Mmax * 2);
   ENS(sorted_entry, pl.Mmax * 4);
@@ -225,7 +233,8 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   ENS(run_head, pl.runs_max * PT_WORDS * 4);
   ENS(run_tail, pl.runs_max * PT_WORDS * 4);
   ENS(head_key, pl.runs_max * 4);
-  ENS(tail_key, pl.runs_max * 4);
+  ENS(tail_next, pl.runs_max * 4);
+  ENS(fix_list, (pl.runs_max / ACC_THREADS + 2) * 8 + 8);
   ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_out, (size_t)d.W * pl.nterms * 32 * 4 + 64);
@@ -245,33 +254,54 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   };
   mark(PH_START);
   HIPCHECK(hipMemsetAsync(c->err.p, 0, 16, s));
-  HIPCHECK(hipMemsetAsync(c->coarse_count.p, 0, (size_t)d.nbins * 4, s));
+  HIPCHECK(hipMemsetAsync(c->fix_list.p, 0, 4, s));
   hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
                      c->err.as<uint32_t>());
   mark(PH_PREPARE);
-  const unsigned sgrid = grid_for(d.n, 256 * d.spt);
-  const size_t lds = (size_t)d.nbins * 4;
-  hipLaunchKernelGGL(k_recode_count, dim3(sgrid), dim3(256), lds, s, d_scalars, d, c->coarse_count.as<uint32_t>());
+  if (d.c <= 16) {
+    hipLaunchKernelGGL(k_recode_digits<uint16_t>, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_scalars, d,
+                       c->digits.as<uint16_t>());
+  } else {
+    hipLaunchKernelGGL(k_recode_digits<uint32_t>, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_scalars, d,
+                       c->digits.as<uint32_t>());
+  }
   mark(PH_RECODE);
-  hipLaunchKernelGGL(k_coarse_scan, dim3(1), dim3(1024), 0, s, c->coarse_count.as<uint32_t>(),
-                     c->coarse_base.as<uint32_t>(), c->coarse_cursor.as<uint32_t>(), d.nbins);
+  if (d.c <= 16) {
+    hipLaunchKernelGGL(k_part_hist<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 4, s,
+                       c->digits.as<uint16_t>(), d, c->hist_rows.as<uint32_t>());
+  } else {
+    hipLaunchKernelGGL(k_part_hist<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 4, s,
+                       c->digits.as<uint32_t>(), d, c->hist_rows.as<uint32_t>());
+  }
+  hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, c->hist_rows.as<uint32_t>(), d,
+                     c->rel.as<uint32_t>(), c->colsum.as<uint32_t>());
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, c->colsum.as<uint32_t>(), c->bin_base.as<uint32_t>(),
+                     d.nbins);
   mark(PH_SCAN);
-  hipLaunchKernelGGL(k_coarse_scatter, dim3(sgrid), dim3(256), lds, s, d_scalars, d, c->coarse_cursor.as<uint32_t>(),
-                     c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+  if (d.c <= 16) {
+    hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                       c->digits.as<uint16_t>(), d, c->hist_rows.as<uint32_t>(), c->rel.as<uint32_t>(),
+                       c->bin_base.as<uint32_t>(), c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+  } else {
+    hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                       c->digits.as<uint32_t>(), d, c->hist_rows.as<uint32_t>(), c->rel.as<uint32_t>(),
+                       c->bin_base.as<uint32_t>(), c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+  }
   mark(PH_SCATTER);
-  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(256), 0, s, c->part_entry.as<uint32_t>(),
-                     c->part_fine.as<uint16_t>(), c->coarse_base.as<uint32_t>(), d, c->sorted_entry.as<uint32_t>(),
+  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, c->part_entry.as<uint32_t>(),
+                     c->part_fine.as<uint16_t>(), c->bin_base.as<uint32_t>(), d, c->sorted_entry.as<uint32_t>(),
                      c->sorted_key.as<uint32_t>(), c->bucket_count.as<uint32_t>());
   mark(PH_FINE);
-  const uint32_t* total = c->coarse_base.as<uint32_t>() + d.nbins;
-  const unsigned rgrid = grid_for(pl.runs_max, 256);
-  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(256), 0, s, c->pts.as<uint32_t>(), c->sorted_entry.as<uint32_t>(),
-                     c->sorted_key.as<uint32_t>(), total, pl.K, c->buckets.as<uint32_t>(), c->run_head.as<uint32_t>(),
-                     c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(), c->tail_key.as<uint32_t>());
+  const uint32_t* total = c->bin_base.as<uint32_t>() + d.nbins;
+  const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
+  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, c->pts.as<uint32_t>(),
+                     c->sorted_entry.as<uint32_t>(), c->sorted_key.as<uint32_t>(), total, pl.K, c->buckets.as<uint32_t>(),
+                     c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
+                     c->tail_next.as<uint32_t>(), c->fix_list.as<uint32_t>());
   mark(PH_ACCUM);
-  hipLaunchKernelGGL(k_fixup, dim3(rgrid), dim3(256), 0, s, total, pl.K, c->run_head.as<uint32_t>(),
-                     c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(), c->tail_key.as<uint32_t>(),
-                     c->buckets.as<uint32_t>());
+  hipLaunchKernelGGL(k_fixup, dim3(grid_for(rgrid, 64)), dim3(64), 0, s, c->fix_list.as<uint32_t>(), total, pl.K,
+                     c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
+                     c->tail_next.as<uint32_t>(), c->buckets.as<uint32_t>());
   mark(PH_FIXUP);
   hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
                      c->buckets.as<uint32_t>(), c->bucket_count.as<uint32_t>(), d, pl.L, c->red_U.as<uint32_t>(),
@@ -448,9 +478,9 @@ void msm_shutdown(void) {
     hipGetDevice(&prev);
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->coarse_count, &c->coarse_base,
-                   &c->coarse_cursor, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->sorted_key,
-                   &c->bucket_count, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_key,
+    Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->digits, &c->hist_rows, &c->rel, &c->colsum,
+                   &c->bin_base, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->sorted_key,
+                   &c->bucket_count, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_next, &c->fix_list,
                    &c->red_U, &c->red_T, &c->red_out};
     for (Buf* b : bufs) b->release();
     c->h_out.release();

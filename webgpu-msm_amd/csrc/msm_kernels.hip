@@ -5,15 +5,17 @@
 //
 //   k_prepare_points   wire points (BE x|y|t|z, 128 B) -> precomputed affine (y-x, y+x, 2dt) in
 //                      29-bit Montgomery limbs, 128 B records (one cache line each)
-//   k_recode_count     signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
-//                      LDS histogram of (window, coarse bucket range)
-//   k_coarse_scan      exclusive scan of the coarse histogram (one workgroup)
-//   k_coarse_scatter   digits -> coarse bins (per-WG reservation, write runs stay contiguous)
+//   k_recode_digits    signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
+//                      written window-major (= first sort level: one contiguous array per window)
+//   k_part_hist        per (window, chunk) LDS histogram over the window's coarse bucket ranges
+//   k_part_colscan     column prefix sums of the histogram rows -> each chunk's slice of every bin
+//   k_bin_scan         exclusive scan of the bin totals (one workgroup)
+//   k_part_scatter     digits -> coarse bins (each chunk writes its own contiguous slice per bin)
 //   k_fine_sort        one WG per coarse bin: LDS counting sort by bucket -> globally sorted
 //                      (entry, bucket key) list + per-bucket counts
 //   k_accumulate       fixed-length runs of the sorted list, one lane per run: mixed adds, whole
-//                      buckets written directly, run-boundary pieces written as head/tail partials
-//   k_fixup            joins head/tail partials of buckets that straddle runs
+//                      buckets written directly, buckets cut by run boundaries joined through LDS
+//   k_fixup            joins the few cut buckets whose run chain crosses a workgroup
 //   k_bucket_reduce_1  per (window, chunk of L buckets): running sums -> U_c = sum (i+1) B, T_c = sum B
 //   k_bucket_reduce_2  per (window, term): plain sums R_{w,V} = sum_c U_c, R_{w,k} = sum_{c: bit k} T_c,
 //                      converted to canonical standard form for the host Horner
@@ -119,21 +121,19 @@ __device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32
 // ---------------------------------------------------------------------------------------------
 // scalar recoding
 // ---------------------------------------------------------------------------------------------
-// Raw c-bit window w of a 256-bit little-endian scalar (bits beyond 255 read as zero).
-__device__ __forceinline__ uint32_t window_bits(const uint32_t s[8], uint32_t lo_bit, uint32_t c) {
-  uint32_t wi = lo_bit >> 5, sh = lo_bit & 31;
-  uint32_t lo = wi < 8 ? (s[wi] >> sh) : 0u;
-  uint32_t hi = (sh != 0 && wi + 1 < 8) ? (s[wi + 1] << (32 - sh)) : 0u;
-  return (lo | hi) & ((1u << c) - 1u);
-}
-
-// Signed recoding of one scalar.  Calls f(window, digit) for every window, digit in
-// [-(2^(c-1)-1), 2^(c-1)]; sum_w digit_w 2^(c w) == scalar exactly (W = ceil(257/c) windows).
+// Signed recoding of one scalar (little-endian words, consumed in place).  Calls f(window, digit)
+// for every window, digit in [-(2^(c-1)-1), 2^(c-1)]; sum_w digit_w 2^(c w) == scalar exactly
+// (W = ceil(257/c) windows).  The scalar is shifted down c bits per window with v_alignbit so no
+// register array is ever indexed dynamically (that would spill it to scratch).
 template <typename F>
-__device__ __forceinline__ void recode(const uint32_t s[8], const MsmDims& d, F&& f) {
+__device__ __forceinline__ void recode(uint32_t s[8], const MsmDims& d, F&& f) {
+  const uint32_t mask = (1u << d.c) - 1u;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < d.W; w++) {
-    uint32_t v = window_bits(s, w * d.c, d.c) + carry;
+    const uint32_t v = (s[0] & mask) + carry;
+#pragma unroll
+    for (int q = 0; q < 7; q++) s[q] = __builtin_amdgcn_alignbit(s[q + 1], s[q], d.c);
+    s[7] >>= d.c;
     int32_t digit;
     if (v > d.B) {
       digit = (int32_t)v - (int32_t)(2 * d.B);
@@ -150,42 +150,130 @@ __device__ __forceinline__ void load_scalar(const uint32_t* __restrict__ scalars
   load_be_words(scalars + (size_t)i * 8, s);
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_recode_count(const uint32_t* __restrict__ scalars, MsmDims d,
-                                                                 uint32_t* __restrict__ coarse_count) {
-  extern __shared__ uint32_t lds_hist[];
-  for (uint32_t b = threadIdx.x; b < d.nbins; b += blockDim.x) lds_hist[b] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * (blockDim.x * d.spt);
-  for (uint32_t k = 0; k < d.spt; k++) {
-    uint32_t i = base + k * blockDim.x + threadIdx.x;
-    if (i >= d.n) break;
-    uint32_t s[8];
-    load_scalar(scalars, i, s);
-    recode(s, d, [&](uint32_t w, int32_t digit) {
-      if (digit != 0) {
-        uint32_t b = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
-        atomicAdd(&lds_hist[w * d.nbc + (b >> d.fb)], 1u);
-      }
-    });
+// Wave-level exclusive scan of one u32 per lane (64 lanes); returns the exclusive prefix and sets
+// `total` to the wave sum.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < d.nbins; b += blockDim.x) {
-    uint32_t h = lds_hist[b];
-    if (h) atomicAdd(&coarse_count[b], h);
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// Exclusive scan of cnt[0..nf) in LDS by the first wave of the workgroup (nf <= 64 * per).
+__device__ __forceinline__ void lds_excl_scan_wave0(uint32_t* cnt, uint32_t nf) {
+  if (threadIdx.x < 64) {
+    const uint32_t per = (nf + 63) / 64;
+    const uint32_t lo = threadIdx.x * per;
+    uint32_t local = 0;
+    for (uint32_t k = 0; k < per; k++)
+      if (lo + k < nf) local += cnt[lo + k];
+    uint32_t tot;
+    uint32_t run = wave_excl_scan(local, tot);
+    for (uint32_t k = 0; k < per; k++) {
+      if (lo + k < nf) {
+        const uint32_t c = cnt[lo + k];
+        cnt[lo + k] = run;
+        run += c;
+      }
+    }
   }
 }
 
-// Exclusive scan of coarse_count[0..nbins) into coarse_base[0..nbins] (coarse_base[nbins] = total);
-// coarse_cursor gets a copy of the bases.  One workgroup of 1024 threads.
-extern "C" __global__ void __launch_bounds__(1024) k_coarse_scan(const uint32_t* __restrict__ coarse_count,
-                                                                 uint32_t* __restrict__ coarse_base,
-                                                                 uint32_t* __restrict__ coarse_cursor, uint32_t nbins) {
+// Digit codes, window-major digits[w][i]: bucket b = |d| - 1 plus a sign bit, or ZERO.
+//   c <= 16: uint16_t, sign = bit 15, ZERO = 0xffff (b = 0x7fff with the sign set would be
+//            d = -2^15, which signed recoding never produces)
+//   c >  16: uint32_t, sign = bit 31, ZERO = 0xffffffff
+template <typename T>
+struct DigitCode;
+template <>
+struct DigitCode<uint16_t> {
+  static constexpr uint32_t ZERO = 0xffffu, SIGN = 0x8000u, MAG = 0x7fffu, SHIFT = 15;
+};
+template <>
+struct DigitCode<uint32_t> {
+  static constexpr uint32_t ZERO = 0xffffffffu, SIGN = 0x80000000u, MAG = 0x7fffffffu, SHIFT = 31;
+};
+
+// Pass 0: recode every scalar once into window-major digit codes.  The window-major layout is the
+// first sort level for free: each window is one contiguous array.
+template <typename T>
+__global__ void __launch_bounds__(256) k_recode_digits(const uint32_t* __restrict__ scalars, MsmDims d,
+                                                       T* __restrict__ digits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.n) return;
+  uint32_t s[8];
+  load_scalar(scalars, i, s);
+  recode(s, d, [&](uint32_t w, int32_t digit) {
+    uint32_t code = DigitCode<T>::ZERO;
+    if (digit != 0) code = ((uint32_t)(digit < 0 ? -digit : digit) - 1u) | (digit < 0 ? DigitCode<T>::SIGN : 0u);
+    digits[(size_t)w * d.n + i] = (T)code;
+  });
+}
+
+// Pass 1: per (window, chunk) histogram over the window's nbc coarse bins -> hist_rows[w][chunk][bin].
+constexpr uint32_t PT_THREADS = 1024;
+template <typename T>
+__global__ void __launch_bounds__(PT_THREADS) k_part_hist(const T* __restrict__ digits, MsmDims d,
+                                                          uint32_t* __restrict__ hist_rows) {
+  extern __shared__ uint32_t lds_hist[];
+  const uint32_t w = blockIdx.y, ck = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lds_hist[b] = 0;
+  __syncthreads();
+  const T* dw = digits + (size_t)w * d.n;
+  const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += PT_THREADS) {
+    const uint32_t code = dw[i];
+    if (code != DigitCode<T>::ZERO) atomicAdd(&lds_hist[(code & DigitCode<T>::MAG) >> d.fb], 1u);
+  }
+  __syncthreads();
+  uint32_t* row = hist_rows + ((size_t)w * d.nch + ck) * d.nbc;
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) row[b] = lds_hist[b];
+}
+
+// Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
+// colsum[w * nbc + bin] = column total.  One workgroup per (64 bins, window); 16 waves split chunks.
+extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t* __restrict__ hist_rows, MsmDims d,
+                                                                  uint32_t* __restrict__ rel,
+                                                                  uint32_t* __restrict__ colsum) {
+  __shared__ uint32_t wsum[16][64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.y;
+  const uint32_t bin = blockIdx.x * 64 + lane;
+  const uint32_t rows = (d.nch + 15) / 16;
+  const uint32_t r0 = wave * rows, r1 = min(d.nch, r0 + rows);
+  const size_t base = (size_t)w * d.nch * d.nbc;
+  uint32_t sum = 0;
+  if (bin < d.nbc)
+    for (uint32_t r = r0; r < r1; r++) sum += hist_rows[base + (size_t)r * d.nbc + bin];
+  wsum[wave][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t v = 0; v < wave; v++) run += wsum[v][lane];
+  if (bin < d.nbc) {
+    for (uint32_t r = r0; r < r1; r++) {
+      const size_t at = base + (size_t)r * d.nbc + bin;
+      const uint32_t h = hist_rows[at];
+      rel[at] = run;
+      run += h;
+    }
+    if (wave == 15) colsum[w * d.nbc + bin] = run;
+  }
+}
+
+// Exclusive scan of colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] = total entries).
+extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ colsum,
+                                                              uint32_t* __restrict__ bin_base, uint32_t nbins) {
   __shared__ uint32_t part[1024];
   const uint32_t per = (nbins + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per;
   uint32_t sum = 0;
   for (uint32_t k = 0; k < per; k++)
-    if (lo + k < nbins) sum += coarse_count[lo + k];
+    if (lo + k < nbins) sum += colsum[lo + k];
   part[threadIdx.x] = sum;
   __syncthreads();
   for (uint32_t off = 1; off < 1024; off <<= 1) {
@@ -194,109 +282,151 @@ extern "C" __global__ void __launch_bounds__(1024) k_coarse_scan(const uint32_t*
     part[threadIdx.x] += v;
     __syncthreads();
   }
-  uint32_t run = part[threadIdx.x] - sum;  // exclusive prefix
+  uint32_t run = part[threadIdx.x] - sum;
   for (uint32_t k = 0; k < per; k++) {
     if (lo + k < nbins) {
-      coarse_base[lo + k] = run;
-      coarse_cursor[lo + k] = run;
-      run += coarse_count[lo + k];
+      bin_base[lo + k] = run;
+      run += colsum[lo + k];
     }
   }
-  if (threadIdx.x == 1023) coarse_base[nbins] = part[1023];
+  if (threadIdx.x == 1023) bin_base[nbins] = part[1023];
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_coarse_scatter(const uint32_t* __restrict__ scalars, MsmDims d,
-                                                                   uint32_t* __restrict__ coarse_cursor,
-                                                                   uint32_t* __restrict__ part_entry,
-                                                                   uint16_t* __restrict__ part_fine) {
-  extern __shared__ uint32_t lds_hist[];
-  for (uint32_t b = threadIdx.x; b < d.nbins; b += blockDim.x) lds_hist[b] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * (blockDim.x * d.spt);
-  for (uint32_t k = 0; k < d.spt; k++) {
-    uint32_t i = base + k * blockDim.x + threadIdx.x;
-    if (i >= d.n) break;
-    uint32_t s[8];
-    load_scalar(scalars, i, s);
-    recode(s, d, [&](uint32_t w, int32_t digit) {
-      if (digit != 0) {
-        uint32_t b = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
-        atomicAdd(&lds_hist[w * d.nbc + (b >> d.fb)], 1u);
-      }
-    });
+// Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
+// coarse bin.  The chunk is first counting-sorted by bin inside LDS, then streamed out so that
+// consecutive lanes write consecutive addresses of a slice (>= 64 entries per slice by
+// construction of ch): whole lines, one CU each.
+constexpr uint32_t PS_R = 16;  // digits per lane (ch <= PT_THREADS * PS_R)
+template <typename T>
+__global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
+                                                                        const uint32_t* __restrict__ hist_rows,
+                                                                        const uint32_t* __restrict__ rel,
+                                                                        const uint32_t* __restrict__ bin_base,
+                                                                        uint32_t* __restrict__ part_entry,
+                                                                        uint16_t* __restrict__ part_fine) {
+  __shared__ uint32_t st_entry[PT_THREADS * PS_R];
+  __shared__ uint16_t st_fine[PT_THREADS * PS_R];
+  __shared__ uint16_t st_bin[PT_THREADS * PS_R];
+  extern __shared__ uint32_t dyn[];  // [nbc] local cursor, [nbc] local start, [nbc] global slice start
+  uint32_t* lcur = dyn;
+  uint32_t* lstart = dyn + d.nbc;
+  uint32_t* gstart = dyn + 2 * d.nbc;
+  const uint32_t w = blockIdx.y, ck = blockIdx.x;
+  const size_t row = ((size_t)w * d.nch + ck) * d.nbc;
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
+    lcur[b] = hist_rows[row + b];
+    gstart[b] = bin_base[w * d.nbc + b] + rel[row + b];
   }
   __syncthreads();
-  // reserve this workgroup's slice of every coarse bin it touches
-  for (uint32_t b = threadIdx.x; b < d.nbins; b += blockDim.x) {
-    uint32_t h = lds_hist[b];
-    lds_hist[b] = h ? atomicAdd(&coarse_cursor[b], h) : 0u;
-  }
+  lds_excl_scan_wave0(lcur, d.nbc);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lstart[b] = lcur[b];
   __syncthreads();
   const uint32_t fmask = (1u << d.fb) - 1u;
-  for (uint32_t k = 0; k < d.spt; k++) {
-    uint32_t i = base + k * blockDim.x + threadIdx.x;
-    if (i >= d.n) break;
-    uint32_t s[8];
-    load_scalar(scalars, i, s);
-    recode(s, d, [&](uint32_t w, int32_t digit) {
-      if (digit != 0) {
-        uint32_t b = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
-        uint32_t pos = atomicAdd(&lds_hist[w * d.nbc + (b >> d.fb)], 1u);
-        part_entry[pos] = (i << 1) | (digit < 0 ? 1u : 0u);
-        part_fine[pos] = (uint16_t)(b & fmask);
-      }
-    });
+  const T* dw = digits + (size_t)w * d.n;
+  const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
+  uint32_t code[PS_R];
+#pragma unroll
+  for (uint32_t r = 0; r < PS_R; r++) {
+    const uint32_t i = lo + r * PT_THREADS + threadIdx.x;
+    code[r] = i < hi ? (uint32_t)dw[i] : DigitCode<T>::ZERO;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < PS_R; r++) {
+    if (code[r] != DigitCode<T>::ZERO) {
+      const uint32_t i = lo + r * PT_THREADS + threadIdx.x;
+      const uint32_t b = code[r] & DigitCode<T>::MAG;
+      const uint32_t bin = b >> d.fb;
+      const uint32_t p = atomicAdd(&lcur[bin], 1u);
+      st_entry[p] = (i << 1) | (code[r] >> DigitCode<T>::SHIFT);
+      st_fine[p] = (uint16_t)(b & fmask);
+      st_bin[p] = (uint16_t)bin;
+    }
+  }
+  __syncthreads();
+  const uint32_t m = lcur[d.nbc - 1];  // past-the-end of the last bin = live digits of the chunk
+  for (uint32_t j = threadIdx.x; j < m; j += PT_THREADS) {
+    const uint32_t bin = st_bin[j];
+    const uint32_t dst = gstart[bin] + (j - lstart[bin]);
+    part_entry[dst] = st_entry[j];
+    part_fine[dst] = st_fine[j];
   }
 }
 
-// One workgroup per coarse bin: counting sort of the bin's entries by fine bucket.
-extern "C" __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ part_entry,
-                                                              const uint16_t* __restrict__ part_fine,
-                                                              const uint32_t* __restrict__ coarse_base, MsmDims d,
-                                                              uint32_t* __restrict__ sorted_entry,
-                                                              uint32_t* __restrict__ sorted_key,
-                                                              uint32_t* __restrict__ bucket_count) {
-  __shared__ uint32_t cnt[512];
-  __shared__ uint32_t scan_tmp[256];
+// Pass 3: one workgroup per coarse bin, counting sort by fine bucket (<= FS_MAXF per bin).  A bin
+// of at most FS_CAP entries is sorted inside LDS and streamed out coalesced; larger bins (skewed
+// scalars) loop over register tiles and scatter directly.
+constexpr uint32_t FS_THREADS = 256;
+constexpr uint32_t FS_R = 24;
+constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS
+constexpr uint32_t FS_MAXF = 2048;
+
+extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint32_t* __restrict__ part_entry,
+                                                                     const uint16_t* __restrict__ part_fine,
+                                                                     const uint32_t* __restrict__ bin_base, MsmDims d,
+                                                                     uint32_t* __restrict__ sorted_entry,
+                                                                     uint32_t* __restrict__ sorted_key,
+                                                                     uint32_t* __restrict__ bucket_count) {
+  __shared__ uint32_t cnt[FS_MAXF];
+  __shared__ uint32_t st_entry[FS_CAP];
+  __shared__ uint16_t st_fine[FS_CAP];
   const uint32_t bin = blockIdx.x;
   const uint32_t nf = 1u << d.fb;
-  const uint32_t base = coarse_base[bin];
-  const uint32_t m = coarse_base[bin + 1] - base;
+  const uint32_t base = bin_base[bin];
+  const uint32_t m = bin_base[bin + 1] - base;
   const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
   const uint32_t key0 = w * d.B + (cb << d.fb);
-  for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cnt[f] = 0;
+  for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < m; e += blockDim.x) atomicAdd(&cnt[part_fine[base + e]], 1u);
+  const bool staged = m <= FS_CAP;
+  uint32_t fk[FS_R], en[FS_R];
+  for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
+#pragma unroll
+    for (uint32_t r = 0; r < FS_R; r++) {
+      const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
+      fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+      en[r] = (staged && e < m) ? part_entry[base + e] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < FS_R; r++)
+      if (fk[r] != 0xffffu) atomicAdd(&cnt[fk[r]], 1u);
+  }
   __syncthreads();
-  // exclusive scan of cnt[0..nf) (nf <= 512: two values per thread)
-  uint32_t c0 = 0, c1 = 0;
-  const uint32_t f0 = 2 * threadIdx.x, f1 = 2 * threadIdx.x + 1;
-  if (f0 < nf) c0 = cnt[f0];
-  if (f1 < nf) c1 = cnt[f1];
-  scan_tmp[threadIdx.x] = c0 + c1;
+  for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) bucket_count[key0 + f] = cnt[f];
   __syncthreads();
-  for (uint32_t off = 1; off < 256; off <<= 1) {
-    uint32_t v = threadIdx.x >= off ? scan_tmp[threadIdx.x - off] : 0u;
+  lds_excl_scan_wave0(cnt, nf);
+  __syncthreads();
+  if (staged) {
+#pragma unroll
+    for (uint32_t r = 0; r < FS_R; r++) {
+      if (fk[r] != 0xffffu) {
+        const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
+        st_entry[p] = en[r];
+        st_fine[p] = (uint16_t)fk[r];
+      }
+    }
     __syncthreads();
-    scan_tmp[threadIdx.x] += v;
-    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) {
+      sorted_entry[base + j] = st_entry[j];
+      sorted_key[base + j] = key0 + st_fine[j];
+    }
+    return;
   }
-  uint32_t ex = scan_tmp[threadIdx.x] - (c0 + c1);
-  __syncthreads();
-  if (f0 < nf) {
-    bucket_count[key0 + f0] = c0;
-    cnt[f0] = ex;
-  }
-  if (f1 < nf) {
-    bucket_count[key0 + f1] = c1;
-    cnt[f1] = ex + c0;
-  }
-  __syncthreads();
-  for (uint32_t e = threadIdx.x; e < m; e += blockDim.x) {
-    uint32_t f = part_fine[base + e];
-    uint32_t pos = base + atomicAdd(&cnt[f], 1u);
-    sorted_entry[pos] = part_entry[base + e];
-    sorted_key[pos] = key0 + f;
+  for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
+#pragma unroll
+    for (uint32_t r = 0; r < FS_R; r++) {
+      const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
+      fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+      en[r] = e < m ? part_entry[base + e] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < FS_R; r++) {
+      if (fk[r] != 0xffffu) {
+        const uint32_t pos = base + atomicAdd(&cnt[fk[r]], 1u);
+        sorted_entry[pos] = en[r];
+        sorted_key[pos] = key0 + fk[r];
+      }
+    }
   }
 }
 
@@ -335,78 +465,146 @@ __device__ __forceinline__ xyzt load_pt(const uint32_t* __restrict__ src) {
   return p;
 }
 
-// Write one finished segment of the sorted list.  Whole buckets go straight to the bucket table;
-// a segment cut by the run start (head) or run end (tail) goes to the run's partial slots.
-__device__ __forceinline__ void flush_segment(const xyzt& acc, uint32_t key, bool is_head, bool is_tail, uint32_t t,
-                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ run_head,
-                                              uint32_t* __restrict__ run_tail, uint32_t* __restrict__ head_key,
-                                              uint32_t* __restrict__ tail_key) {
-  if (is_head) {
-    store_pt(run_head + (size_t)t * PT_WORDS, acc);
-    head_key[t] = key | (is_tail ? KEY_PASS : 0u);
-  } else if (is_tail) {
-    store_pt(run_tail + (size_t)t * PT_WORDS, acc);
-    tail_key[t] = key;
-  } else {
-    store_pt(buckets + (size_t)key * PT_WORDS, acc);
+__device__ __forceinline__ void store_pt_lds(uint32_t* dst, const xyzt& p) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    dst[k] = p.X.v[k];
+    dst[NL + k] = p.Y.v[k];
+    dst[2 * NL + k] = p.T.v[k];
+    dst[3 * NL + k] = p.Z.v[k];
   }
 }
-
-extern "C" __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ pts,
-                                                               const uint32_t* __restrict__ sorted_entry,
-                                                               const uint32_t* __restrict__ sorted_key,
-                                                               const uint32_t* __restrict__ total_ptr, uint32_t K,
-                                                               uint32_t* __restrict__ buckets,
-                                                               uint32_t* __restrict__ run_head,
-                                                               uint32_t* __restrict__ run_tail,
-                                                               uint32_t* __restrict__ head_key,
-                                                               uint32_t* __restrict__ tail_key) {
-  const uint32_t M = *total_ptr;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t s = t * K;
-  if (s >= M) return;
-  const uint32_t e = min(s + K, M);
-  head_key[t] = KEY_INVALID;
-  tail_key[t] = KEY_INVALID;
-  uint32_t cur = sorted_key[s];
-  const bool started_before = s > 0 && sorted_key[s - 1] == cur;
-  bool seg_first = true;
-  xyzt acc = pt_identity();
-  for (uint32_t pos = s; pos < e; pos++) {
-    uint32_t k = sorted_key[pos];
-    if (k != cur) {
-      flush_segment(acc, cur, seg_first && started_before, false, t, buckets, run_head, run_tail, head_key, tail_key);
-      acc = pt_identity();
-      cur = k;
-      seg_first = false;
-    }
-    uint32_t ent = sorted_entry[pos];
-    pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
-    acc = pt_madd(acc, q);
+__device__ __forceinline__ xyzt load_pt_lds(const uint32_t* src) {
+  xyzt p;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    p.X.v[k] = src[k];
+    p.Y.v[k] = src[NL + k];
+    p.T.v[k] = src[2 * NL + k];
+    p.Z.v[k] = src[3 * NL + k];
   }
-  const bool cont = e < M && sorted_key[e] == cur;
-  flush_segment(acc, cur, seg_first && started_before, cont, t, buckets, run_head, run_tail, head_key, tail_key);
+  return p;
 }
 
-// Joins a bucket cut across runs: tail partial of run t + head partials of runs t+1.. (pass-through
-// runs continue the chain).
-extern "C" __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_ptr, uint32_t K,
-                                                          const uint32_t* __restrict__ run_head,
-                                                          const uint32_t* __restrict__ run_tail,
-                                                          const uint32_t* __restrict__ head_key,
-                                                          const uint32_t* __restrict__ tail_key,
-                                                          uint32_t* __restrict__ buckets) {
+// Bucket accumulation over the sorted list.  Lane = run of K consecutive entries (perfect load
+// balance whatever the bucket sizes).  Inside a run, whole buckets are written straight to the
+// bucket table.  A bucket cut by run boundaries is joined without a second pass over HBM: every
+// run's leading piece (head) is staged in LDS, and after one barrier the run where the bucket
+// starts adds its trailing piece (tail) to the heads of the following runs of the same workgroup.
+// Only a chain leaving the workgroup goes to k_fixup (via a short list).
+constexpr uint32_t ACC_THREADS = 256;
+extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
+                                                                       const uint32_t* __restrict__ sorted_entry,
+                                                                       const uint32_t* __restrict__ sorted_key,
+                                                                       const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                                                       uint32_t* __restrict__ buckets,
+                                                                       uint32_t* __restrict__ run_head,
+                                                                       uint32_t* __restrict__ run_tail,
+                                                                       uint32_t* __restrict__ head_key,
+                                                                       uint32_t* __restrict__ tail_next,
+                                                                       uint32_t* __restrict__ fix_list) {
+  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
+  __shared__ uint32_t sh_hkey[ACC_THREADS];
   const uint32_t M = *total_ptr;
   const uint32_t nruns = (M + K - 1) / K;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nruns) return;
-  const uint32_t key = tail_key[t];
-  if (key == KEY_INVALID) return;
+  const uint32_t lt = threadIdx.x;
+  const uint32_t t = blockIdx.x * ACC_THREADS + lt;
+  const uint32_t s = t * K;
+  sh_hkey[lt] = KEY_INVALID;
+  xyzt acc = pt_identity();
+  uint32_t cur = KEY_INVALID;
+  bool has_tail = false;
+  if (s < M) {
+    const uint32_t e = min(s + K, M);
+    cur = sorted_key[s];
+    const bool started_before = s > 0 && sorted_key[s - 1] == cur;
+    bool seg_first = true;
+    for (uint32_t pos = s; pos < e; pos++) {
+      const uint32_t k = sorted_key[pos];
+      if (k != cur) {
+        if (seg_first && started_before) {
+          store_pt_lds(sh_head[lt], acc);
+          sh_hkey[lt] = cur;
+        } else {
+          store_pt(buckets + (size_t)cur * PT_WORDS, acc);
+        }
+        acc = pt_identity();
+        cur = k;
+        seg_first = false;
+      }
+      const uint32_t ent = sorted_entry[pos];
+      pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
+      acc = pt_madd(acc, q);
+    }
+    const bool cont = e < M && sorted_key[e] == cur;
+    if (seg_first && started_before) {  // the whole run belongs to a bucket begun earlier
+      store_pt_lds(sh_head[lt], acc);
+      sh_hkey[lt] = cur | (cont ? KEY_PASS : 0u);
+    } else if (cont) {
+      has_tail = true;  // acc = tail piece of bucket `cur`
+    } else {
+      store_pt(buckets + (size_t)cur * PT_WORDS, acc);
+    }
+  }
+  __syncthreads();
+  // Heads that a chain from the previous workgroup may need: runs preceded (within this WG) only
+  // by pass-through runs.  Normally just lane 0.
+  if (s < M && sh_hkey[lt] != KEY_INVALID) {
+    bool reachable = true;
+    for (uint32_t v = 0; v < lt; v++) {
+      const uint32_t hv = sh_hkey[v];
+      if (hv == KEY_INVALID || !(hv & KEY_PASS)) {
+        reachable = false;
+        break;
+      }
+    }
+    if (reachable) {
+      store_pt(run_head + (size_t)t * PT_WORDS, load_pt_lds(sh_head[lt]));
+      head_key[t] = sh_hkey[lt];
+    }
+  }
+  if (has_tail) {
+    uint32_t lu = lt + 1;
+    bool done = false;
+    while (lu < ACC_THREADS && blockIdx.x * ACC_THREADS + lu < nruns) {
+      const uint32_t hk = sh_hkey[lu];
+      acc = pt_add(acc, load_pt_lds(sh_head[lu]));
+      if (!(hk & KEY_PASS)) {
+        done = true;
+        break;
+      }
+      lu++;
+    }
+    if (done) {
+      store_pt(buckets + (size_t)cur * PT_WORDS, acc);
+    } else {  // chain continues into the next workgroup's runs
+      store_pt(run_tail + (size_t)t * PT_WORDS, acc);
+      tail_next[t] = blockIdx.x * ACC_THREADS + lu;
+      const uint32_t slot = atomicAdd(&fix_list[0], 1u);
+      fix_list[1 + 2 * slot] = t;
+      fix_list[2 + 2 * slot] = cur;
+    }
+  }
+}
+
+// Finishes the (rare) buckets whose run chain crosses a workgroup boundary: tail piece + heads of
+// the next workgroup's leading runs (pass-through runs continue the chain).
+extern "C" __global__ void __launch_bounds__(64) k_fixup(const uint32_t* __restrict__ fix_list,
+                                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                                         const uint32_t* __restrict__ run_head,
+                                                         const uint32_t* __restrict__ run_tail,
+                                                         const uint32_t* __restrict__ head_key,
+                                                         const uint32_t* __restrict__ tail_next,
+                                                         uint32_t* __restrict__ buckets) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= fix_list[0]) return;
+  const uint32_t nruns = (*total_ptr + K - 1) / K;
+  const uint32_t t = fix_list[1 + 2 * i], key = fix_list[2 + 2 * i];
   xyzt acc = load_pt(run_tail + (size_t)t * PT_WORDS);
-  for (uint32_t u = t + 1; u < nruns; u++) {
+  for (uint32_t u = tail_next[t]; u < nruns; u++) {
     acc = pt_add(acc, load_pt(run_head + (size_t)u * PT_WORDS));
     const uint32_t hk = head_key[u];
-    if (hk == KEY_INVALID || !(hk & KEY_PASS)) break;
+    if (!(hk & KEY_PASS)) break;
   }
   store_pt(buckets + (size_t)key * PT_WORDS, acc);
 }
