@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--run-length", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-logn", type=int, default=16)
+    ap.add_argument("--cpu-sample-logn", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
 

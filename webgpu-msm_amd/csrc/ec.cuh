@@ -32,12 +32,12 @@ __device__ __forceinline__ xyzt pt_identity() {
 
 // acc + q (q affine precomputed).  add-2008-hwcd-3 with Z2 = 1, k = 2d.  All outputs normalised.
 __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);  // N*N
-  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);  // S*N
-  fe C = fe_mul(p.T, q.kt);                // N*N
-  fe D = fe_dbl_n(p.Z);                    // N
-  fe E = fe_sub(B, A);                     // N
-  fe F = fe_sub(D, C);                     // N
+  fe A = fe_mul(fe_sub_u(p.Y, p.X), q.ymx);  // U*N
+  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);    // S*N
+  fe C = fe_mul(p.T, q.kt);                  // N*N
+  fe D = fe_dbl_n(p.Z);                      // N
+  fe E = fe_sub_u(B, A);                     // U (meets F: N and H: S only)
+  fe F = fe_sub(D, C);                       // N
   fe G = fe_add(D, C);                     // S
   fe H = fe_add(B, A);                     // S
   xyzt r;
@@ -50,11 +50,11 @@ __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
 
 // p + q, both extended projective.  add-2008-hwcd-3, k = 2d: 9M.
 __device__ __forceinline__ xyzt pt_add(const xyzt& p, const xyzt& q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), fe_sub(q.Y, q.X));
+  fe A = fe_mul(fe_sub_u(p.Y, p.X), fe_sub(q.Y, q.X));  // U*N
   fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));  // S*S
   fe C = fe_mul(fe_mul(p.T, q.T), fe_const(K2D29));
   fe D = fe_dbl_n(fe_mul(p.Z, q.Z));
-  fe E = fe_sub(B, A);
+  fe E = fe_sub_u(B, A);
   fe F = fe_sub(D, C);
   fe G = fe_add(D, C);
   fe H = fe_add(B, A);

@@ -45,6 +45,10 @@ __device__ constexpr uint32_t K2D29[NL] = {534219742u, 493355007u, 360522798u, 7
 // 2d*R^2 mod p: fe_mul(t_std, K2D_R2) = Montgomery form of 2d*t straight from standard form.
 __device__ constexpr uint32_t K2D_R2_29[NL] = {22956135u, 32535989u, 128498189u, 216570651u, 307994937u,
                                                462062068u, 55188476u, 243732681u, 295952u};
+// 2^256 mod p (standard form): fe_mul(a_mont, R256_29) = a * 2^256 mod p, i.e. the host's
+// 4x64-bit Montgomery representation (hostfield.h, R = 2^256) of a.
+__device__ constexpr uint32_t R256_29[NL] = {536870899u, 149159935u, 536870047u, 267001567u, 16705317u,
+                                             180005014u, 175397728u, 105215859u, 871386u};
 // 8p in a redundant form with limbs 0..7 >= 2^29-1, so (a + K8P - b) never goes negative limb-wise
 // for normalised b.
 __device__ constexpr uint32_t K8P29[NL] = {536870920u, 610271231u, 536871443u, 661646591u, 939568340u,
@@ -72,18 +76,26 @@ __device__ __forceinline__ fe fe_zero() {
 __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 
 // Montgomery product a*b*2^-261 mod p (result normalised, value < 2p when a,b < 2^257).
+// Reduction digit m' = 2^29 - (column mod 2^29) in [1, 2^29] instead of the textbook
+// (-column) mod 2^29: it still zeroes the column, and the carry it produces is always exactly
+// (column >> 29) + 1, so the nine "+1"s are pre-seeded into columns 1..9 and each step needs no
+// 64-bit "column += m" (saves a zero-extension move and a half-rate 64-bit add per step).
+// Column bound with the larger digit: <= 0.95 * 2^64 for unnormalised-sub x S operands
+// (tests/golden bounds check).
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   uint64_t c[2 * NL];
+  c[0] = 0;
 #pragma unroll
-  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
+  for (int k = 1; k <= NL; k++) c[k] = 1;
+#pragma unroll
+  for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
 #pragma unroll
   for (int i = 0; i < NL; i++)
 #pragma unroll
     for (int j = 0; j < NL; j++) c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
 #pragma unroll
   for (int i = 0; i < NL; i++) {
-    uint32_t m = (0u - (uint32_t)c[i]) & LMASK;
-    c[i] += m;  // m * p_0, p_0 == 1: low 29 bits of c[i] become zero
+    const uint32_t m = (1u << LBITS) - ((uint32_t)c[i] & LMASK);
     c[i + 1] += c[i] >> LBITS;
 #pragma unroll
     for (int j = 1; j < NL; j++) c[i + j] = mad64(m, P29[j], c[i + j]);
@@ -136,6 +148,14 @@ __device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
 #pragma unroll
   for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + K8P29[i] - b.v[i];
   fe_norm(r);
+  return r;
+}
+// a - b + 8p without renormalisation ("U": limbs < 1.48 * 2^30).  Legal as one fe_mul operand
+// against an N or S operand (column bound 0.95 * 2^64), never U*U.
+__device__ __forceinline__ fe fe_sub_u(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + K8P29[i] - b.v[i];
   return r;
 }
 // -b (= 8p - b), normalised.
@@ -209,6 +229,14 @@ __device__ __forceinline__ fe fe_to_std(const fe& a) {
   fe one = fe_zero();
   one.v[0] = 1;
   fe r = fe_mul(a, one);  // value <= p
+  fe_norm(r);
+  if (fe_geq_p(r)) r = fe_sub_p(r);
+  return r;
+}
+
+// Device Montgomery form -> canonical host Montgomery form (a * 2^256 mod p, in [0, p)).
+__device__ __forceinline__ fe fe_to_host_mont(const fe& a) {
+  fe r = fe_mul(a, fe_const(R256_29));  // value < p + small: one conditional subtraction
   fe_norm(r);
   if (fe_geq_p(r)) r = fe_sub_p(r);
   return r;

@@ -102,6 +102,7 @@ struct HostBuf {
 
 struct DevCtx {
   int device = -1;
+  int n_cu = 256;
   hipStream_t stream = nullptr;
   std::mutex mu;
   Buf wire_points, wire_scalars, pts, err, digits, hist_rows, rel, colsum, bin_base;
@@ -154,6 +155,9 @@ int get_ctx(int device, DevCtx** out) {
       return MSM_ERR_HIP;
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->n_cu = prop.multiProcessorCount;
     hipSetDevice(prev);
     g_ctx[device] = c;
   }
@@ -179,7 +183,7 @@ uint32_t ilog2(uint32_t v) {
   return r;
 }
 
-int make_plan(size_t n, const msm_opts* o, Plan* pl) {
+int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
   uint32_t c = (o && o->window_bits) ? o->window_bits : msm_best_window(n);
   if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
   if (n >= (1ull << 30)) return MSM_ERR_INVALID_ARG;
@@ -320,29 +324,30 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
 }
 
 // Host tail: MSM = sum_w 2^(c w) [ R_{w,V} + sum_k 2^(lgL + k) R_{w,k} ]  (Horner over bit positions).
-// Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then into_affine.
+// Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then into_affine.  The
+// device already emitted the terms in this file's Montgomery form (fe_to_host_mont).
 Pt horner_tail(const Plan& pl, const uint32_t* terms) {
   const MsmDims& d = pl.d;
-  const uint32_t maxpos = d.c * (d.W - 1) + pl.lgL + (pl.nterms - 1);
-  std::vector<std::vector<Pt>> at(maxpos + 1);
-  for (uint32_t w = 0; w < d.W; w++) {
-    for (uint32_t t = 0; t < pl.nterms; t++) {
-      const uint32_t* o = terms + ((size_t)w * pl.nterms + t) * 32;
-      Pt p;
-      p.X = fq_from_std(reinterpret_cast<const uint64_t*>(o));
-      p.Y = fq_from_std(reinterpret_cast<const uint64_t*>(o + 8));
-      p.T = fq_from_std(reinterpret_cast<const uint64_t*>(o + 16));
-      p.Z = fq_from_std(reinterpret_cast<const uint64_t*>(o + 24));
-      if (fq_is_zero(p.X) && fq_eq(p.Y, p.Z)) continue;  // identity
-      uint32_t pos = d.c * w + (t == 0 ? 0 : pl.lgL + (t - 1));
-      at[pos].push_back(p);
-    }
-  }
+  const int maxpos = (int)(d.c * (d.W - 1) + pl.lgL + (pl.nterms - 1));
   Pt acc = pt_identity();
   bool live = false;
-  for (int pos = (int)maxpos; pos >= 0; pos--) {
+  for (int pos = maxpos; pos >= 0; pos--) {
     if (live) acc = pt_dbl(acc);
-    for (const Pt& p : at[pos]) {
+    // terms landing on this bit position: window w = pos / c with offset r = pos % c
+    const uint32_t w = (uint32_t)pos / d.c, r = (uint32_t)pos % d.c;
+    if (w >= d.W) continue;
+    uint32_t t_idx[2];
+    int nt = 0;
+    if (r == 0) t_idx[nt++] = 0;
+    if (r >= pl.lgL && r - pl.lgL + 1 < pl.nterms) t_idx[nt++] = r - pl.lgL + 1;
+    for (int q = 0; q < nt; q++) {
+      const uint32_t* o = terms + ((size_t)w * pl.nterms + t_idx[q]) * 32;
+      Pt p;
+      memcpy(p.X.l, o, 32);
+      memcpy(p.Y.l, o + 8, 32);
+      memcpy(p.T.l, o + 16, 32);
+      memcpy(p.Z.l, o + 24, 32);
+      if (fq_is_zero(p.X) && fq_eq(p.Y, p.Z)) continue;  // identity
       acc = live ? pt_add(acc, p) : p;
       live = true;
     }
@@ -385,7 +390,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
     return MSM_OK;
   }
   Plan pl;
-  int rc = make_plan(n, o, &pl);
+  int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
   if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
   hipStream_t s = user_stream ? user_stream : c->stream;

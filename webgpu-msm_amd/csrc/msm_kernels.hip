@@ -11,11 +11,10 @@
 //   k_part_colscan     column prefix sums of the histogram rows -> each chunk's slice of every bin
 //   k_bin_scan         exclusive scan of the bin totals (one workgroup)
 //   k_part_scatter     digits -> coarse bins (each chunk writes its own contiguous slice per bin)
-//   k_fine_sort        one WG per coarse bin: LDS counting sort by bucket -> globally sorted
-//                      (entry, bucket key) list + per-bucket counts
-//   k_accumulate       fixed-length runs of the sorted list, one lane per run: mixed adds, whole
-//                      buckets written directly, buckets cut by run boundaries joined through LDS
-//   k_fixup            joins the few cut buckets whose run chain crosses a workgroup
+//   k_fine_sort        per coarse bin: LDS counting sort by bucket -> (entry, bucket key) lists
+//   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
+//                      written directly, buckets cut by run boundaries joined through LDS
+//   k_fixup            the few buckets whose run chain crosses a workgroup boundary
 //   k_bucket_reduce_1  per (window, chunk of L buckets): running sums -> U_c = sum (i+1) B, T_c = sum B
 //   k_bucket_reduce_2  per (window, term): plain sums R_{w,V} = sum_c U_c, R_{w,k} = sum_{c: bit k} T_c,
 //                      converted to canonical standard form for the host Horner
@@ -641,8 +640,9 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
 }
 
 // One workgroup per (window, term).  term 0: R_V = sum_c U_c; term 1+k: R_k = sum_{c: bit k of c} T_c.
-// Output: X, Y, T, Z in canonical standard form (8 LE words each) for the host.
-constexpr int RED2_THREADS = 256;
+// Output: X, Y, T, Z in the host's Montgomery form (a * 2^256 mod p, 8 LE words each), so the
+// host Horner (hostfield.h) uses them without conversion.
+constexpr int RED2_THREADS = 1024;
 extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(const uint32_t* __restrict__ in_U,
                                                                              const uint32_t* __restrict__ in_T,
                                                                              uint32_t nchunks, uint32_t nterms,
@@ -669,7 +669,7 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
   }
   if (threadIdx.x == 0) {
     uint32_t* o = out_std + (size_t)blockIdx.x * 32;
-    fe c4[4] = {fe_to_std(acc.X), fe_to_std(acc.Y), fe_to_std(acc.T), fe_to_std(acc.Z)};
+    fe c4[4] = {fe_to_host_mont(acc.X), fe_to_host_mont(acc.Y), fe_to_host_mont(acc.T), fe_to_host_mont(acc.Z)};
 #pragma unroll
     for (int q = 0; q < 4; q++) fe_to_words_le(c4[q], o + 8 * q);
   }

@@ -28,7 +28,8 @@ __all__ = [
 P = 8444461749428370424248824938781546531375899335154063827935233455917409239041
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "_lib", "libmsm.so")
+# MSM_AMD_LIB selects an alternative in-tree build (kernel A/B experiments); default libmsm.so
+_LIB = os.environ.get("MSM_AMD_LIB") or os.path.join(_HERE, "_lib", "libmsm.so")
 
 
 class MsmError(RuntimeError):
