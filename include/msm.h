@@ -102,7 +102,9 @@ uint32_t msm_split_windows(uint32_t window_bits);
 int msm_gen_points(const uint32_t g_xy_be[16], uint64_t k0, uint64_t step, size_t n, uint32_t* points_be);
 int msm_gen_scalars(uint64_t seed, size_t n, uint32_t* scalars_be);
 
-/* Profiling (hipEvents around every phase). */
+/* Profiling.  enable = 0: off; 1: hipEvents between every phase (launches go eagerly, no graph
+ * replay); 2: k_accumulate and the device total only (events between graph replays, so the
+ * timed path is the production one).  msm_last_profile reports the calling thread's device. */
 int msm_set_profiling(int enable);
 int msm_last_profile(msm_profile_t* out);
 

@@ -1,0 +1,158 @@
+"""Static limb-bound proof for the device field/curve code (webgpu-msm_amd/csrc/fp29.cuh, ec.cuh).
+
+The 29-bit-limb lazy Montgomery multiply accumulates up to 18 partial products per 64-bit column
+with no carry handling, and the curve formulas feed unnormalised sums/differences into it.  A
+column overflow would be a silent, data-dependent wrong answer that random tests hit almost
+never, so this test walks every formula in the kernels with per-limb worst-case bounds (interval
+arithmetic on the limb maxima) and asserts:
+
+  * every fe_mul column stays < 2^64 (products + reduction terms + seed + incoming carry);
+  * every fe_mul operand pair keeps a*b < p * 2^261, so the lazy result is < 2p (no final
+    subtraction needed);
+  * fe_sub / fe_neg never produce a negative limb (K8P dominates the subtrahend limb-wise).
+
+It mirrors the kernels by hand: when a formula in ec.cuh changes, change it here too.
+"""
+P = 8444461749428370424248824938781546531375899335154063827935233455917409239041
+NL, LB = 9, 29
+MASK = (1 << LB) - 1
+R = 1 << 261
+P29 = [(P >> (LB * i)) & MASK for i in range(NL)]
+K8P29 = [536870920, 610271231, 536871443, 661646591, 939568340, 880373981, 718018184, 1050291364, 9788201]
+
+
+class B:
+    """Worst-case limb maxima + value maximum of a field element."""
+
+    def __init__(self, limbs, value):
+        self.l = list(limbs)
+        self.v = value
+
+    @staticmethod
+    def normalised(value):
+        top = value >> (LB * (NL - 1))
+        return B([MASK] * (NL - 1) + [top], value)
+
+
+N_MUL = B.normalised(2 * P)  # fe_mul output: normalised, value < 2p
+
+
+def value_of(limbs):
+    return sum(x << (LB * i) for i, x in enumerate(limbs))
+
+
+def fe_mul(a: B, b: B) -> B:
+    assert a.v * b.v < P * R, "lazy Montgomery output would exceed 2p"
+    cols = [0] * (2 * NL)
+    for i in range(NL):
+        for j in range(NL):
+            cols[i + j] += a.l[i] * b.l[j]
+    for k in range(1, NL + 1):
+        cols[k] += 1  # pre-seeded carries
+    carry = 0
+    for k in range(2 * NL):
+        red = 0
+        for i in range(NL):  # reduction digits m_i <= 2^29 times P29[k - i], k - i in 1..8
+            j = k - i
+            if 1 <= j < NL and i < NL:
+                red += (1 << LB) * P29[j]
+        col = cols[k] + red + carry
+        assert col < 1 << 64, f"column {k} may reach {col / 2**64:.3f} * 2^64"
+        carry = (col >> LB) + 1
+    return N_MUL
+
+
+def fe_add(a: B, b: B) -> B:
+    return B([x + y for x, y in zip(a.l, b.l)], a.v + b.v)
+
+
+def fe_sub_u(a: B, b: B) -> B:
+    for i in range(NL):
+        assert K8P29[i] >= b.l[i], "fe_sub: negative limb possible"
+    assert b.v < 8 * P
+    return B([x + k for x, k in zip(a.l, K8P29)], a.v + 8 * P)
+
+
+def fe_norm(a: B) -> B:
+    return B.normalised(a.v)
+
+
+def fe_sub(a: B, b: B) -> B:
+    for i in range(NL - 1):
+        assert a.l[i] < 1 << 30
+    return fe_norm(fe_sub_u(a, b))
+
+
+def fe_neg_u(b: B) -> B:  # pre_neg_if's unnormalised 8p - kt
+    for i in range(NL):
+        assert K8P29[i] >= b.l[i]
+    return B(list(K8P29), 8 * P)
+
+
+# point coordinates are always fe_mul outputs (or the identity's normalised constants)
+PT = dict(X=N_MUL, Y=N_MUL, T=N_MUL, Z=N_MUL)
+ONE29 = 536870474 + (276299775 << 29)  # value of Montgomery one is < p; covered by N_MUL
+
+
+def test_madd_bounds():
+    # pre-point record from k_prepare_points: ymx = fe_sub (normalised), ypx = fe_add_n, kt = fe_mul
+    ymx = fe_sub(N_MUL, N_MUL)
+    ypx = fe_norm(fe_add(N_MUL, N_MUL))
+    kt = N_MUL
+    for neg in (False, True):
+        q_ymx, q_ypx = (ypx, ymx) if neg else (ymx, ypx)
+        q_kt = fe_neg_u(kt) if neg else kt
+        p = PT
+        A = fe_mul(fe_sub_u(p["Y"], p["X"]), q_ymx)
+        Bv = fe_mul(fe_add(p["Y"], p["X"]), q_ypx)
+        C = fe_mul(p["T"], q_kt)
+        D = fe_add(p["Z"], p["Z"])
+        E = fe_sub_u(Bv, A)
+        F = fe_sub(D, C)
+        G = fe_add(D, C)
+        H = fe_add(Bv, A)
+        fe_mul(E, F)
+        fe_mul(G, H)
+        fe_mul(E, H)
+        fe_mul(F, G)
+
+
+def test_padd_bounds():
+    p = q = PT
+    A = fe_mul(fe_sub_u(p["Y"], p["X"]), fe_sub(q["Y"], q["X"]))
+    Bv = fe_mul(fe_add(p["Y"], p["X"]), fe_add(q["Y"], q["X"]))
+    C = fe_mul(fe_mul(p["T"], q["T"]), N_MUL)
+    D0 = fe_mul(p["Z"], q["Z"])
+    D = fe_add(D0, D0)
+    E = fe_sub_u(Bv, A)
+    F = fe_sub(D, C)
+    G = fe_add(D, C)
+    H = fe_add(Bv, A)
+    fe_mul(E, F)
+    fe_mul(G, H)
+    fe_mul(E, H)
+    fe_mul(F, G)
+
+
+def test_pdbl_bounds():
+    p = PT
+    A = fe_mul(p["X"], p["X"])
+    Bv = fe_mul(p["Y"], p["Y"])
+    Z2 = fe_mul(p["Z"], p["Z"])
+    C = fe_norm(fe_add(Z2, Z2))
+    S = fe_mul(fe_add(p["X"], p["Y"]), fe_add(p["X"], p["Y"]))
+    E = fe_sub(fe_sub(S, A), Bv)
+    G = fe_sub(Bv, A)
+    F = fe_sub(G, C)
+    AB = fe_norm(fe_add(A, Bv))
+    H = fe_norm(fe_sub_u(B([0] * NL, 0), AB))
+    fe_mul(E, F)
+    fe_mul(G, H)
+    fe_mul(E, H)
+    fe_mul(F, G)
+
+
+def test_model_matches_header_constants():
+    assert value_of(K8P29) == 8 * P
+    assert all(k >= MASK for k in K8P29[:8])
+    assert P29 == [1, 277610496, 66, 351141280, 452990362, 110046747, 358187729, 198395284, 1223525]

@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU tests, then a tuning sweep.  Stops at the first crash/timeout.
+set -u
+mkdir -p gpurun_out
+run() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -n 4 "gpurun_out/$name.txt" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout 600
+run sweep_L8 300 python tools/sweep.py --windows 16 --runs 32,64
+MSM_RED_L=4 run sweep_L4 300 python tools/sweep.py --windows 16 --runs 64
+MSM_RED_L=16 run sweep_L16 300 python tools/sweep.py --windows 15,16 --runs 64

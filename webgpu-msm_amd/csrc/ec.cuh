@@ -34,12 +34,12 @@ __device__ __forceinline__ xyzt pt_identity() {
 __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
   fe A = fe_mul(fe_sub_u(p.Y, p.X), q.ymx);  // U*N
   fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);    // S*N
-  fe C = fe_mul(p.T, q.kt);                  // N*N
-  fe D = fe_dbl_n(p.Z);                      // N
+  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*U for a negated q, pre_neg_if)
+  fe D = fe_add(p.Z, p.Z);                   // 2N: limbs < 2^30, left unnormalised
   fe E = fe_sub_u(B, A);                     // U (meets F: N and H: S only)
   fe F = fe_sub(D, C);                       // N
-  fe G = fe_add(D, C);                     // S
-  fe H = fe_add(B, A);                     // S
+  fe G = fe_add(D, C);                       // 2N + N: limbs < 1.5 * 2^30 (meets H: S and F: N only)
+  fe H = fe_add(B, A);                       // S
   xyzt r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
@@ -53,7 +53,8 @@ __device__ __forceinline__ xyzt pt_add(const xyzt& p, const xyzt& q) {
   fe A = fe_mul(fe_sub_u(p.Y, p.X), fe_sub(q.Y, q.X));  // U*N
   fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));  // S*S
   fe C = fe_mul(fe_mul(p.T, q.T), fe_const(K2D29));
-  fe D = fe_dbl_n(fe_mul(p.Z, q.Z));
+  fe D = fe_mul(p.Z, q.Z);
+  D = fe_add(D, D);  // 2N, unnormalised (see pt_madd)
   fe E = fe_sub_u(B, A);
   fe F = fe_sub(D, C);
   fe G = fe_add(D, C);
@@ -92,11 +93,14 @@ __device__ __forceinline__ xyzt pt_neg(const xyzt& p) {
   return r;
 }
 
+// -q = (-x, y): swap (y - x, y + x) and negate 2dt.  The negated kt = 8p - kt is left
+// unnormalised (U form, limbs < 2^30), legal as pt_madd's C = T * kt operand (N * U).
 __device__ __forceinline__ pre pre_neg_if(const pre& q, bool neg) {
   pre r;
   r.ymx = fe_sel(neg, q.ymx, q.ypx);
   r.ypx = fe_sel(neg, q.ypx, q.ymx);
-  r.kt = fe_sel(neg, q.kt, fe_neg(q.kt));
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.kt.v[i] = neg ? K8P29[i] - q.kt.v[i] : q.kt.v[i];
   return r;
 }
 

@@ -58,6 +58,17 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * b + c;
 }
 
+#ifndef MSM_SEED_ASM
+#define MSM_SEED_ASM 1
+#endif
+// a * b + 1 as one v_mad_u64_u32 with an inline-constant addend (carry-out discarded into an
+// unused SGPR pair).
+__device__ __forceinline__ uint64_t mad64_seed1(uint32_t a, uint32_t b) {
+  uint64_t r, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 1" : "=v"(r), "=s"(unused) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ void fe_set(fe& r, const uint32_t* c) {
 #pragma unroll
   for (int i = 0; i < NL; i++) r.v[i] = c[i];
@@ -84,6 +95,23 @@ __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 // (tests/golden bounds check).
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   uint64_t c[2 * NL];
+#if MSM_SEED_ASM
+  // The first product of each seeded column carries the +1 as its inline-constant addend.  In
+  // plain C, LLVM reassociates the constant out of the accumulation chain into a separate 64-bit
+  // add per column; the asm result is opaque, so the chain stays put.
+#pragma unroll
+  for (int k = 0; k < NL; k++) c[k] = k == 0 ? (uint64_t)a.v[0] * b.v[0] : mad64_seed1(a.v[0], b.v[k]);
+  c[NL] = mad64_seed1(a.v[1], b.v[NL - 1]);
+#pragma unroll
+  for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++)
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+      if (i == 0 || (i == 1 && j == NL - 1)) continue;  // already issued as seeded products
+      c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
+    }
+#else
   c[0] = 0;
 #pragma unroll
   for (int k = 1; k <= NL; k++) c[k] = 1;
@@ -93,6 +121,7 @@ __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   for (int i = 0; i < NL; i++)
 #pragma unroll
     for (int j = 0; j < NL; j++) c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
+#endif
 #pragma unroll
   for (int i = 0; i < NL; i++) {
     const uint32_t m = (1u << LBITS) - ((uint32_t)c[i] & LMASK);

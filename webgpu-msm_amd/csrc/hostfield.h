@@ -8,6 +8,7 @@
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#include <x86intrin.h>
 
 namespace msmh {
 
@@ -43,33 +44,62 @@ static inline void sub_p(uint64_t a[4]) {
   }
 }
 
+// CIOS Montgomery multiply with explicit add-with-carry chains (adc/adcx under -madx); about
+// 1.7x faster than the u128-accumulator form under clang.  Inputs < p, output < p.
+typedef unsigned long long ull;
+static inline ull mul_lohi(ull a, ull b, ull* hi) {
+  u128 r = (u128)a * b;
+  *hi = (ull)(r >> 64);
+  return (ull)r;
+}
 static inline Fq fq_mul(const Fq& a, const Fq& b) {
-  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  const ull b0 = b.l[0], b1 = b.l[1], b2 = b.l[2], b3 = b.l[3];
+  ull t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
   for (int i = 0; i < 4; i++) {
-    u128 c = 0;
-    for (int j = 0; j < 4; j++) {
-      c += (u128)a.l[i] * b.l[j] + t[j];
-      t[j] = (uint64_t)c;
-      c >>= 64;
-    }
-    u128 s = (u128)t[4] + (uint64_t)c;
-    t[4] = (uint64_t)s;
-    t[5] = (uint64_t)(s >> 64);
-    uint64_t m = t[0] * NP;
-    c = (u128)m * P[0] + t[0];
-    c >>= 64;
-    for (int j = 1; j < 4; j++) {
-      c += (u128)m * P[j] + t[j];
-      t[j - 1] = (uint64_t)c;
-      c >>= 64;
-    }
-    s = (u128)t[4] + (uint64_t)c;
-    t[3] = (uint64_t)s;
-    t[4] = t[5] + (uint64_t)(s >> 64);
+    const ull ai = a.l[i];
+    ull h0, h1, h2, h3;
+    const ull l0 = mul_lohi(ai, b0, &h0), l1 = mul_lohi(ai, b1, &h1);
+    const ull l2 = mul_lohi(ai, b2, &h2), l3 = mul_lohi(ai, b3, &h3);
+    unsigned char c = 0;
+    c = _addcarry_u64(c, t0, l0, &t0);
+    c = _addcarry_u64(c, t1, l1, &t1);
+    c = _addcarry_u64(c, t2, l2, &t2);
+    c = _addcarry_u64(c, t3, l3, &t3);
+    c = _addcarry_u64(c, t4, 0, &t4);
+    ull t5 = c;
+    c = _addcarry_u64(0, t1, h0, &t1);
+    c = _addcarry_u64(c, t2, h1, &t2);
+    c = _addcarry_u64(c, t3, h2, &t3);
+    c = _addcarry_u64(c, t4, h3, &t4);
+    t5 += c;
+    const ull m = t0 * NP;
+    const ull m0 = mul_lohi(m, P[0], &h0), m1 = mul_lohi(m, P[1], &h1);
+    const ull m2 = mul_lohi(m, P[2], &h2), m3 = mul_lohi(m, P[3], &h3);
+    ull drop;
+    c = _addcarry_u64(0, t0, m0, &drop);
+    c = _addcarry_u64(c, t1, m1, &t0);
+    c = _addcarry_u64(c, t2, m2, &t1);
+    c = _addcarry_u64(c, t3, m3, &t2);
+    c = _addcarry_u64(c, t4, 0, &t3);
+    t5 += c;
+    c = _addcarry_u64(0, t0, h0, &t0);
+    c = _addcarry_u64(c, t1, h1, &t1);
+    c = _addcarry_u64(c, t2, h2, &t2);
+    c = _addcarry_u64(c, t3, h3, &t3);
+    t4 = t5 + c;
   }
+  // a, b < p < 2^253: the CIOS result is < 2p < 2^254, so t4 == 0 and one subtraction suffices
+  ull d0, d1, d2, d3;
+  unsigned char br = _subborrow_u64(0, t0, P[0], &d0);
+  br = _subborrow_u64(br, t1, P[1], &d1);
+  br = _subborrow_u64(br, t2, P[2], &d2);
+  br = _subborrow_u64(br, t3, P[3], &d3);
   Fq r;
-  memcpy(r.l, t, 32);
-  if (t[4] || geq_p(r.l)) sub_p(r.l);
+  if (br) {
+    r.l[0] = t0, r.l[1] = t1, r.l[2] = t2, r.l[3] = t3;
+  } else {
+    r.l[0] = d0, r.l[1] = d1, r.l[2] = d2, r.l[3] = d3;
+  }
   return r;
 }
 static inline Fq fq_add(const Fq& a, const Fq& b) {
@@ -152,14 +182,16 @@ struct Pt {
 };
 static inline Pt pt_identity() { return Pt{fq_zero(), fq_one(), fq_zero(), fq_one()}; }
 
-static inline Pt pt_add(const Pt& p, const Pt& q) {
+// p + q; with want_t = false the result's T is left stale (fine when a doubling comes next:
+// dbl-2008-hwcd never reads T).
+static inline Pt pt_add(const Pt& p, const Pt& q, bool want_t = true) {
   Fq A = fq_mul(fq_sub(p.Y, p.X), fq_sub(q.Y, q.X));
   Fq B = fq_mul(fq_add(p.Y, p.X), fq_add(q.Y, q.X));
   Fq C = fq_mul(fq_mul(p.T, q.T), Fq{{K2D_M[0], K2D_M[1], K2D_M[2], K2D_M[3]}});
   Fq D = fq_mul(p.Z, q.Z);
   D = fq_add(D, D);
   Fq E = fq_sub(B, A), F = fq_sub(D, C), G = fq_add(D, C), H = fq_add(B, A);
-  return Pt{fq_mul(E, F), fq_mul(G, H), fq_mul(E, H), fq_mul(F, G)};
+  return Pt{fq_mul(E, F), fq_mul(G, H), want_t ? fq_mul(E, H) : fq_zero(), fq_mul(F, G)};
 }
 static inline Pt pt_dbl(const Pt& p) {
   Fq A = fq_mul(p.X, p.X);
@@ -173,6 +205,26 @@ static inline Pt pt_dbl(const Pt& p) {
   Fq F = fq_sub(G, C);
   Fq H = fq_sub(fq_zero(), fq_add(A, B));
   return Pt{fq_mul(E, F), fq_mul(G, H), fq_mul(E, H), fq_mul(F, G)};
+}
+// 2^k * p.  dbl-2008-hwcd never reads T, so every doubling but the last skips T3 = E*H.
+static inline Pt pt_dbl_n(Pt p, int k) {
+  for (int i = 0; i < k; i++) {
+    Fq A = fq_mul(p.X, p.X);
+    Fq B = fq_mul(p.Y, p.Y);
+    Fq C = fq_mul(p.Z, p.Z);
+    C = fq_add(C, C);
+    Fq S = fq_add(p.X, p.Y);
+    S = fq_mul(S, S);
+    Fq E = fq_sub(fq_sub(S, A), B);
+    Fq G = fq_sub(B, A);
+    Fq F = fq_sub(G, C);
+    Fq H = fq_sub(fq_zero(), fq_add(A, B));
+    p.X = fq_mul(E, F);
+    p.Y = fq_mul(G, H);
+    p.Z = fq_mul(F, G);
+    if (i == k - 1) p.T = fq_mul(E, H);
+  }
+  return p;
 }
 // affine (x, y) in standard form; identity -> (0, 1)
 static inline void pt_to_affine_std(const Pt& p, uint64_t x[4], uint64_t y[4]) {

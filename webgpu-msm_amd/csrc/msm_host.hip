@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -51,11 +52,14 @@ enum Phase {
   PH_COUNT
 };
 
+uint64_t g_alloc_gen = 0;  // bumped on every (re)allocation: captured graphs hold raw pointers
+
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return MSM_OK;
+    g_alloc_gen++;
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -83,9 +87,13 @@ struct HostBuf {
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return MSM_OK;
+    g_alloc_gen++;
     if (p) hipHostFree(p);
     p = nullptr;
     cap = 0;
+    // pinned, host-cacheable memory; k_bucket_reduce_2 writes its results straight into it and
+    // publishes them with __threadfence_system() (a coherent/uncached mapping would make the
+    // host Horner's reads ~4x slower)
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
       p = nullptr;
       return MSM_ERR_OOM;
@@ -106,17 +114,33 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   Buf wire_points, wire_scalars, pts, err, digits, hist_rows, rel, colsum, bin_base;
-  Buf part_entry, part_fine, sorted_entry, sorted_key, bucket_count, buckets;
-  Buf run_head, run_tail, head_key, tail_next, fix_list, red_U, red_T, red_out;
-  HostBuf h_out;
+  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
+  Buf run_head, run_tail, head_key, tail_next, fix_list, red_U, red_T;
+  HostBuf h_out;         // k_bucket_reduce_2 writes the window terms, err and total here
+  void* h_out_dev = nullptr;
   hipEvent_t ev[PH_COUNT] = {};
-  bool profiling = false;
+  int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate only (graph-friendly)
+  // The launch sequence of the last MSM shape, captured once into a HIP graph and replayed:
+  // one hipGraphLaunch instead of ~14 enqueues per MSM.
+  struct GraphKey {
+    const void *pts, *sc;
+    size_t n;
+    uint32_t c, K, L;
+    int prof;
+    uint64_t gen;
+    bool operator==(const GraphKey& o) const {
+      return pts == o.pts && sc == o.sc && n == o.n && c == o.c && K == o.K && L == o.L && prof == o.prof &&
+             gen == o.gen;
+    }
+  } gkey{};
+  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};  // whole MSM, or pre / - / post
+  bool graphs_ok = true;
   msm_profile_t last{};
 };
 
 std::mutex g_mu;
 std::vector<DevCtx*> g_ctx;
-bool g_profiling = false;
+int g_profiling = 0;
 int g_ndev = -1;
 
 int probe_devices() {
@@ -172,7 +196,8 @@ struct Plan {
   uint32_t L;       // bucket-reduce chunk length
   uint32_t lgL;
   uint32_t nchunks; // B / L
-  uint32_t nterms;  // 1 + log2(nchunks)
+  uint32_t nv;      // V-slices: R_V = sum_c U_c is split into nv equal partial sums
+  uint32_t nterms;  // nv + log2(nchunks)
   size_t Mmax;      // W * n upper bound on sorted entries
   size_t runs_max;
 };
@@ -203,12 +228,21 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
   pl->d = d;
-  pl->K = (o && o->run_length) ? o->run_length : 32;
+  // Run length: long enough to amortise the per-run head/tail joins, short enough to leave
+  // ~4 waves per SIMD (262144 lanes) of accumulation work.
+  uint32_t kauto = 64;
+  while (kauto > 16 && (size_t)d.W * n / kauto < 262144) kauto >>= 1;
+  pl->K = (o && o->run_length) ? o->run_length : kauto;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
-  pl->L = std::min<uint32_t>(8, d.B);
+  uint32_t L = 8;
+  if (const char* e = getenv("MSM_RED_L")) L = (uint32_t)atoi(e);  // tuning override (power of 2)
+  if (L < 1 || (L & (L - 1))) L = 8;
+  pl->L = std::min<uint32_t>(L, d.B);
   pl->lgL = ilog2(pl->L);
   pl->nchunks = d.B / pl->L;
-  pl->nterms = 1 + ilog2(pl->nchunks);
+  // every k_bucket_reduce_2 workgroup sums at most nchunks/2 points (the R_k terms' size)
+  pl->nv = pl->nchunks >= 2 ? 2 : 1;
+  pl->nterms = pl->nv + ilog2(pl->nchunks);
   pl->Mmax = (size_t)d.W * n;
   pl->runs_max = (pl->Mmax + pl->K - 1) / pl->K + 1;
   if (pl->Mmax >= (1ull << 31)) return MSM_ERR_INVALID_ARG;
@@ -231,8 +265,8 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   ENS(part_entry, pl.Mmax * 4);
   ENS(part_fine, pl.Mmax * 2);
   ENS(sorted_entry, pl.Mmax * 4);
-  ENS(sorted_key, pl.Mmax * 4);
-  ENS(bucket_count, nb * 4);
+  ENS(bucket_start, (nb + 2) * 4);
+  ENS(run_key, pl.runs_max * 4);
   ENS(buckets, nb * PT_WORDS * 4);
   ENS(run_head, pl.runs_max * PT_WORDS * 4);
   ENS(run_tail, pl.runs_max * PT_WORDS * 4);
@@ -241,42 +275,48 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   ENS(fix_list, (pl.runs_max / ACC_THREADS + 2) * 8 + 8);
   ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
-  ENS(red_out, (size_t)d.W * pl.nterms * 32 * 4 + 64);
 #undef ENS
-  if ((rc = c->h_out.ensure((size_t)d.W * pl.nterms * 32 * 4 + 64)) != MSM_OK) return rc;
+  const size_t hbytes = (size_t)d.W * pl.nterms * 32 * 4 + 64;
+  if (hbytes > c->h_out.cap || !c->h_out_dev) {
+    if ((rc = c->h_out.ensure(hbytes)) != MSM_OK) return rc;
+    if (hipHostGetDevicePointer(&c->h_out_dev, c->h_out.p, 0) != hipSuccess) return MSM_ERR_HIP;
+  }
   return MSM_OK;
 }
 
 inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Enqueue the whole device pipeline on `s`; the reduced per-window terms land in c->h_out.
-int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s) {
+// Enqueue (parts of) the device pipeline on `s`; the reduced per-window terms land in c->h_out.
+// PART_PRE: memsets, point preparation and the sort; PART_ACC: bucket accumulation;
+// PART_POST: fixup and bucket reduction.
+constexpr int PART_PRE = 1, PART_ACC = 2, PART_POST = 4, PART_ALL = 7;
+int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s,
+                int parts = PART_ALL) {
   const MsmDims& d = pl.d;
-  const bool prof = c->profiling;
+  const bool prof = c->profiling == 1;
   auto mark = [&](int ph) {
     if (prof) hipEventRecord(c->ev[ph], s);
   };
+  const uint32_t* total = c->bin_base.as<uint32_t>() + d.nbins;
+  const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
+  if (parts & PART_PRE) {
   mark(PH_START);
   HIPCHECK(hipMemsetAsync(c->err.p, 0, 16, s));
   HIPCHECK(hipMemsetAsync(c->fix_list.p, 0, 4, s));
-  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
+  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS)), dim3(PP_THREADS), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
                      c->err.as<uint32_t>());
   mark(PH_PREPARE);
+  const size_t hist_lds = (size_t)d.W * d.nbc * 4;
+  HIPCHECK(hipMemsetAsync(c->hist_rows.p, 0, (size_t)d.nch * d.nbins * 4, s));
+  const unsigned rc_grid = grid_for(d.n, RC_SPAN);
   if (d.c <= 16) {
-    hipLaunchKernelGGL(k_recode_digits<uint16_t>, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_scalars, d,
-                       c->digits.as<uint16_t>());
+    hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+                       c->digits.as<uint16_t>(), c->hist_rows.as<uint32_t>());
   } else {
-    hipLaunchKernelGGL(k_recode_digits<uint32_t>, dim3(grid_for(d.n, 256)), dim3(256), 0, s, d_scalars, d,
-                       c->digits.as<uint32_t>());
+    hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+                       c->digits.as<uint32_t>(), c->hist_rows.as<uint32_t>());
   }
   mark(PH_RECODE);
-  if (d.c <= 16) {
-    hipLaunchKernelGGL(k_part_hist<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 4, s,
-                       c->digits.as<uint16_t>(), d, c->hist_rows.as<uint32_t>());
-  } else {
-    hipLaunchKernelGGL(k_part_hist<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 4, s,
-                       c->digits.as<uint32_t>(), d, c->hist_rows.as<uint32_t>());
-  }
   hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, c->hist_rows.as<uint32_t>(), d,
                      c->rel.as<uint32_t>(), c->colsum.as<uint32_t>());
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, c->colsum.as<uint32_t>(), c->bin_base.as<uint32_t>(),
@@ -293,64 +333,73 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   }
   mark(PH_SCATTER);
   hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, c->part_entry.as<uint32_t>(),
-                     c->part_fine.as<uint16_t>(), c->bin_base.as<uint32_t>(), d, c->sorted_entry.as<uint32_t>(),
-                     c->sorted_key.as<uint32_t>(), c->bucket_count.as<uint32_t>());
+                     c->part_fine.as<uint16_t>(), c->bin_base.as<uint32_t>(), d, pl.K, c->sorted_entry.as<uint32_t>(),
+                     c->bucket_start.as<uint32_t>(), c->run_key.as<uint32_t>());
   mark(PH_FINE);
-  const uint32_t* total = c->bin_base.as<uint32_t>() + d.nbins;
-  const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
+  }
+  if (parts & PART_ACC) {
   hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, c->pts.as<uint32_t>(),
-                     c->sorted_entry.as<uint32_t>(), c->sorted_key.as<uint32_t>(), total, pl.K, c->buckets.as<uint32_t>(),
+                     c->sorted_entry.as<uint32_t>(), c->bucket_start.as<uint32_t>(), c->run_key.as<uint32_t>(), total,
+                     pl.K, c->buckets.as<uint32_t>(),
                      c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
                      c->tail_next.as<uint32_t>(), c->fix_list.as<uint32_t>());
   mark(PH_ACCUM);
+  }
+  if (parts & PART_POST) {
   hipLaunchKernelGGL(k_fixup, dim3(grid_for(rgrid, 64)), dim3(64), 0, s, c->fix_list.as<uint32_t>(), total, pl.K,
                      c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
                      c->tail_next.as<uint32_t>(), c->buckets.as<uint32_t>());
   mark(PH_FIXUP);
   hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
-                     c->buckets.as<uint32_t>(), c->bucket_count.as<uint32_t>(), d, pl.L, c->red_U.as<uint32_t>(),
+                     c->buckets.as<uint32_t>(), c->bucket_start.as<uint32_t>(), d, pl.L, c->red_U.as<uint32_t>(),
                      c->red_T.as<uint32_t>());
   mark(PH_RED1);
   hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, c->red_U.as<uint32_t>(),
-                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nterms, c->red_out.as<uint32_t>());
+                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, c->err.as<uint32_t>(), total,
+                     reinterpret_cast<uint32_t*>(c->h_out_dev));
   mark(PH_RED2);
-  HIPCHECK(hipGetLastError());
-  const size_t outb = (size_t)d.W * pl.nterms * 32 * 4;
-  HIPCHECK(hipMemcpyAsync(c->h_out.p, c->red_out.p, outb, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipMemcpyAsync((char*)c->h_out.p + outb, c->err.p, 4, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipMemcpyAsync((char*)c->h_out.p + outb + 4, total, 4, hipMemcpyDeviceToHost, s));
   mark(PH_READBACK);
+  }
+  HIPCHECK(hipGetLastError());
   return MSM_OK;
 }
 
-// Host tail: MSM = sum_w 2^(c w) [ R_{w,V} + sum_k 2^(lgL + k) R_{w,k} ]  (Horner over bit positions).
-// Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then into_affine.  The
-// device already emitted the terms in this file's Montgomery form (fe_to_host_mont).
+// Host tail: MSM = sum_w 2^(c w) [ sum_v R_{w,v} + sum_k 2^(lgL + k) R_{w,k} ]  (Horner over bit
+// positions).  Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then
+// into_affine.  The device already emitted the terms in this file's Montgomery form
+// (fe_to_host_mont).  Runs of doublings skip T (pt_dbl_proj) except the one feeding an add.
 Pt horner_tail(const Plan& pl, const uint32_t* terms) {
   const MsmDims& d = pl.d;
-  const int maxpos = (int)(d.c * (d.W - 1) + pl.lgL + (pl.nterms - 1));
-  Pt acc = pt_identity();
-  bool live = false;
-  for (int pos = maxpos; pos >= 0; pos--) {
-    if (live) acc = pt_dbl(acc);
-    // terms landing on this bit position: window w = pos / c with offset r = pos % c
-    const uint32_t w = (uint32_t)pos / d.c, r = (uint32_t)pos % d.c;
-    if (w >= d.W) continue;
-    uint32_t t_idx[2];
-    int nt = 0;
-    if (r == 0) t_idx[nt++] = 0;
-    if (r >= pl.lgL && r - pl.lgL + 1 < pl.nterms) t_idx[nt++] = r - pl.lgL + 1;
-    for (int q = 0; q < nt; q++) {
-      const uint32_t* o = terms + ((size_t)w * pl.nterms + t_idx[q]) * 32;
-      Pt p;
-      memcpy(p.X.l, o, 32);
-      memcpy(p.Y.l, o + 8, 32);
-      memcpy(p.T.l, o + 16, 32);
-      memcpy(p.Z.l, o + 24, 32);
-      if (fq_is_zero(p.X) && fq_eq(p.Y, p.Z)) continue;  // identity
-      acc = live ? pt_add(acc, p) : p;
-      live = true;
+  // terms in descending bit position: windows from the top, inside a window R_k from the top
+  // down to the V slices (position 0)
+  std::vector<uint32_t> pos, idx;
+  pos.reserve((size_t)d.W * pl.nterms);
+  idx.reserve((size_t)d.W * pl.nterms);
+  for (int w = (int)d.W - 1; w >= 0; w--)
+    for (int t = (int)pl.nterms - 1; t >= 0; t--) {
+      const uint32_t i = (uint32_t)w * pl.nterms + (uint32_t)t;
+      const uint32_t* o = terms + (size_t)i * 32;
+      Fq X;
+      memcpy(X.l, o, 32);
+      if (fq_is_zero(X) && !memcmp(o + 8, o + 24, 32)) continue;  // identity: X = 0, Y = Z
+      pos.push_back(d.c * (uint32_t)w + ((uint32_t)t < pl.nv ? 0u : pl.lgL + ((uint32_t)t - pl.nv)));
+      idx.push_back(i);
     }
+  Pt acc = pt_identity();
+  if (pos.empty()) return acc;
+  for (size_t j = 0; j < pos.size(); j++) {
+    const uint32_t* o = terms + (size_t)idx[j] * 32;
+    Pt p;
+    memcpy(p.X.l, o, 32);
+    memcpy(p.Y.l, o + 8, 32);
+    memcpy(p.T.l, o + 16, 32);
+    memcpy(p.Z.l, o + 24, 32);
+    // T of the sum is needed when another add follows at the same position, and for the final
+    // result (msm_compute_partial returns X|Y|T|Z); a doubling next never reads it
+    const bool want_t = j + 1 == pos.size() || pos[j + 1] == pos[j];
+    acc = j == 0 ? p : pt_add(acc, p, want_t);
+    const uint32_t next = j + 1 < pos.size() ? pos[j + 1] : 0u;
+    if (pos[j] > next) acc = pt_dbl_n(acc, (int)(pos[j] - next));
   }
   return acc;
 }
@@ -382,6 +431,96 @@ int pt_from_be_xyzt(const uint32_t in[32], Pt* p) {
 
 using clk = std::chrono::steady_clock;
 
+bool graphs_enabled() {
+  static const bool on = !getenv("MSM_NO_GRAPH");
+  return on;
+}
+
+void drop_graphs(DevCtx* c) {
+  for (hipGraphExec_t& g : c->gexec)
+    if (g) {
+      hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+}
+
+int capture(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s, int parts,
+            hipGraphExec_t* out) {
+  hipGraph_t g = nullptr;
+  if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return MSM_ERR_HIP;
+  int rc = enqueue_msm(c, pl, d_points, d_scalars, s, parts);
+  hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc != MSM_OK || e != hipSuccess || !g) {
+    if (g) hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return MSM_ERR_HIP;
+  }
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    (void)hipGetLastError();
+    return MSM_ERR_HIP;
+  }
+  return MSM_OK;
+}
+
+// Enqueue one MSM.  The launch sequence of the last shape is captured into HIP graphs and
+// replayed (one hipGraphLaunch instead of ~14 enqueues).  Profiling mode 1 launches eagerly with
+// an event between every phase; mode 2 brackets an eager k_accumulate launch with events, between
+// two graphs (pre / post).  Captures only on the library's own stream (a caller's stream
+// may be capturing or in use).
+int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s,
+               bool own_stream) {
+  const int prof = c->profiling;
+  const bool graphs = own_stream && c->graphs_ok && graphs_enabled() && prof != 1;
+  if (graphs) {
+    DevCtx::GraphKey key{d_points, d_scalars, (size_t)pl.d.n, pl.d.c, pl.K, pl.L, prof, g_alloc_gen};
+    if (!(c->gexec[0] && key == c->gkey)) {
+      drop_graphs(c);
+      int rc = MSM_OK;
+      if (prof == 2) {
+        rc = capture(c, pl, d_points, d_scalars, s, PART_PRE, &c->gexec[0]);
+        if (rc == MSM_OK) rc = capture(c, pl, d_points, d_scalars, s, PART_POST, &c->gexec[2]);
+      } else {
+        rc = capture(c, pl, d_points, d_scalars, s, PART_ALL, &c->gexec[0]);
+      }
+      if (rc != MSM_OK) {
+        drop_graphs(c);
+        c->graphs_ok = false;  // capture unsupported here: stay eager
+      } else {
+        c->gkey = key;
+      }
+    }
+  }
+  const bool use_graphs = graphs && c->graphs_ok;
+  if (prof == 2) {
+    HIPCHECK(hipEventRecord(c->ev[PH_START], s));
+    if (use_graphs) {
+      HIPCHECK(hipGraphLaunch(c->gexec[0], s));
+    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_PRE)) {
+      return rc;
+    }
+    // k_accumulate itself is launched eagerly between its two events: a graph launch there would
+    // put the graph's own launch latency inside the measured bracket
+    HIPCHECK(hipEventRecord(c->ev[PH_FINE], s));
+    if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_ACC)) return rc;
+    HIPCHECK(hipEventRecord(c->ev[PH_ACCUM], s));
+    if (use_graphs) {
+      HIPCHECK(hipGraphLaunch(c->gexec[2], s));
+    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_POST)) {
+      return rc;
+    }
+    HIPCHECK(hipEventRecord(c->ev[PH_READBACK], s));
+    return MSM_OK;
+  }
+  if (use_graphs) {
+    HIPCHECK(hipGraphLaunch(c->gexec[0], s));
+    return MSM_OK;
+  }
+  return enqueue_msm(c, pl, d_points, d_scalars, s, PART_ALL);
+}
+
 // Run one MSM with device inputs; result as a projective host point.
 int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, size_t n, const msm_opts* o,
                hipStream_t user_stream, Pt* result) {
@@ -394,7 +533,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if (rc != MSM_OK) return rc;
   if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
   hipStream_t s = user_stream ? user_stream : c->stream;
-  if ((rc = enqueue_msm(c, pl, d_points, d_scalars, s)) != MSM_OK) return rc;
+  if ((rc = launch_msm(c, pl, d_points, d_scalars, s, s == c->stream)) != MSM_OK) return rc;
   HIPCHECK(hipStreamSynchronize(s));
   const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
   const uint32_t* h = reinterpret_cast<const uint32_t*>(c->h_out.p);
@@ -407,8 +546,12 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   auto t1 = clk::now();
   if (c->profiling) {
     float ms[PH_COUNT] = {};
-    for (int i = 1; i < PH_COUNT; i++) hipEventElapsedTime(&ms[i], c->ev[i - 1], c->ev[i]);
     msm_profile_t& P = c->last;
+    if (c->profiling == 1) {
+      for (int i = 1; i < PH_COUNT; i++) hipEventElapsedTime(&ms[i], c->ev[i - 1], c->ev[i]);
+    } else {
+      hipEventElapsedTime(&ms[PH_ACCUM], c->ev[PH_FINE], c->ev[PH_ACCUM]);
+    }
     P.prepare_points = ms[PH_PREPARE];
     P.recode_count = ms[PH_RECODE];
     P.coarse_scan = ms[PH_SCAN];
@@ -484,11 +627,13 @@ void msm_shutdown(void) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->digits, &c->hist_rows, &c->rel, &c->colsum,
-                   &c->bin_base, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->sorted_key,
-                   &c->bucket_count, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_next, &c->fix_list,
-                   &c->red_U, &c->red_T, &c->red_out};
+                   &c->bin_base, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->bucket_start,
+                   &c->run_key, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_next, &c->fix_list,
+                   &c->red_U, &c->red_T};
     for (Buf* b : bufs) b->release();
     c->h_out.release();
+    c->h_out_dev = nullptr;
+    drop_graphs(c);
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
     hipSetDevice(prev);
@@ -655,7 +800,7 @@ int msm_split(uint32_t c, const uint32_t* scalars_be, size_t n, uint32_t* out) {
 
 int msm_set_profiling(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
-  g_profiling = enable != 0;
+  g_profiling = enable < 0 ? 0 : enable > 2 ? 1 : enable;
   for (DevCtx* c : g_ctx)
     if (c) c->profiling = g_profiling;
   return MSM_OK;

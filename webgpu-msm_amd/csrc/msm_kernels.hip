@@ -25,6 +25,7 @@
 #include "ec.cuh"
 #include "msm_dev.h"
 
+
 namespace msm {
 
 // ---------------------------------------------------------------------------------------------
@@ -49,19 +50,51 @@ __device__ __forceinline__ fe load_fe(const uint32_t* src) {
   return r;
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_prepare_points(const uint32_t* __restrict__ wire,
-                                                                   uint32_t* __restrict__ pts, uint32_t n,
-                                                                   uint32_t* __restrict__ err) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t* src = wire + (size_t)i * 32;
+// One workgroup = PP_THREADS points.  Wire records and output records (128 B each) move between
+// HBM and LDS with fully coalesced 16-B accesses (a wave covers 1 KiB contiguous per
+// instruction); each lane then works on its own point out of LDS.  The 16-B slots of a record are
+// XOR-swizzled by the record index so the per-lane 128-B-strided LDS reads and writes are free of
+// bank conflicts.
+constexpr uint32_t PP_THREADS = 256;
+__device__ __forceinline__ uint32_t pp_slot(uint32_t rec, uint32_t q) { return rec * 8 + (q ^ (rec & 7)); }
+
+extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(const uint32_t* __restrict__ wire,
+                                                                          uint32_t* __restrict__ pts, uint32_t n,
+                                                                          uint32_t* __restrict__ err) {
+  __shared__ uint4 st[PP_THREADS * 8];
+  const uint32_t p0 = blockIdx.x * PP_THREADS;
+  const uint32_t np = min(PP_THREADS, n - p0);
+  const uint4* src = reinterpret_cast<const uint4*>(wire) + (size_t)p0 * 8;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t g = j * PP_THREADS + threadIdx.x;  // 16-B slot within the block's records
+    if (g < np * 8) st[pp_slot(g >> 3, g & 7)] = src[g];
+  }
+  __syncthreads();
+  const uint32_t i = threadIdx.x;
+  const bool live = i < np;
   uint32_t xw[8], yw[8], tw[8], zw[8];
-  load_be_words(src, xw);
-  load_be_words(src + 8, yw);
-  load_be_words(src + 16, tw);
-  load_be_words(src + 24, zw);
+  if (live) {
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) v[q] = st[pp_slot(i, q)];
+    // big-endian word order: word 0 is the most significant 32 bits (bytes.rs:11-20)
+    uint32_t* dsts[4] = {xw, yw, tw, zw};
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const uint4 a = v[2 * f], b = v[2 * f + 1];
+      uint32_t* le = dsts[f];
+      le[7] = a.x; le[6] = a.y; le[5] = a.z; le[4] = a.w;
+      le[3] = b.x; le[2] = b.y; le[1] = b.z; le[0] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) xw[k] = yw[k] = tw[k] = zw[k] = 0;
+    zw[0] = 1;
+  }
+  __syncthreads();
   bool ok = words_lt_p(xw) && words_lt_p(yw) && words_lt_p(tw) && words_lt_p(zw);
-  if (!ok) atomicOr(err, MSM_DEV_ERR_COORD_RANGE);
+  if (live && !ok) atomicOr(err, MSM_DEV_ERR_COORD_RANGE);
   bool z_one = zw[0] == 1u;
   bool z_zero = zw[0] == 0u;
 #pragma unroll
@@ -69,7 +102,7 @@ extern "C" __global__ void __launch_bounds__(256) k_prepare_points(const uint32_
     z_one = z_one && zw[k] == 0u;
     z_zero = z_zero && zw[k] == 0u;
   }
-  if (z_zero) atomicOr(err, MSM_DEV_ERR_BAD_POINT);
+  if (live && z_zero) atomicOr(err, MSM_DEV_ERR_BAD_POINT);
   fe x = fe_to_mont(fe_from_words_le(xw));
   fe y = fe_to_mont(fe_from_words_le(yw));
   fe kt;
@@ -94,9 +127,16 @@ extern "C" __global__ void __launch_bounds__(256) k_prepare_points(const uint32_
   }
 #pragma unroll
   for (int k = 3 * NL; k < 32; k++) rec[k] = 0;
-  uint4* dst = reinterpret_cast<uint4*>(pts + (size_t)i * 32);
 #pragma unroll
-  for (int k = 0; k < 8; k++) dst[k] = make_uint4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+  for (uint32_t q = 0; q < 8; q++)
+    st[pp_slot(i, q)] = make_uint4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(pts) + (size_t)p0 * 8;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t g = j * PP_THREADS + threadIdx.x;
+    if (g < np * 8) dst[g] = st[pp_slot(g >> 3, g & 7)];
+  }
 }
 
 __device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32_t idx) {
@@ -198,40 +238,45 @@ struct DigitCode<uint32_t> {
   static constexpr uint32_t ZERO = 0xffffffffu, SIGN = 0x80000000u, MAG = 0x7fffffffu, SHIFT = 31;
 };
 
-// Pass 0: recode every scalar once into window-major digit codes.  The window-major layout is the
-// first sort level for free: each window is one contiguous array.
-template <typename T>
-__global__ void __launch_bounds__(256) k_recode_digits(const uint32_t* __restrict__ scalars, MsmDims d,
-                                                       T* __restrict__ digits) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.n) return;
-  uint32_t s[8];
-  load_scalar(scalars, i, s);
-  recode(s, d, [&](uint32_t w, int32_t digit) {
-    uint32_t code = DigitCode<T>::ZERO;
-    if (digit != 0) code = ((uint32_t)(digit < 0 ? -digit : digit) - 1u) | (digit < 0 ? DigitCode<T>::SIGN : 0u);
-    digits[(size_t)w * d.n + i] = (T)code;
-  });
-}
-
-// Pass 1: per (window, chunk) histogram over the window's nbc coarse bins -> hist_rows[w][chunk][bin].
+// Pass 0+1 (fused): each workgroup recodes RC_SPAN scalars (a quarter of one partition chunk of
+// `ch`) into window-major digit codes (the window-major layout is the first sort level for free:
+// each window is one contiguous array) and builds, in LDS, their histogram over every window's
+// nbc coarse bins, flushed with global atomics into hist_rows[w][chunk][bin] (zeroed first).
+// Digits are read back only once, by k_part_scatter.
 constexpr uint32_t PT_THREADS = 1024;
+constexpr uint32_t PS_R = 16;  // digits per lane (ch = PT_THREADS * PS_R)
+constexpr uint32_t RC_THREADS = 1024;
+constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup (4 per lane)
 template <typename T>
-__global__ void __launch_bounds__(PT_THREADS) k_part_hist(const T* __restrict__ digits, MsmDims d,
-                                                          uint32_t* __restrict__ hist_rows) {
-  extern __shared__ uint32_t lds_hist[];
-  const uint32_t w = blockIdx.y, ck = blockIdx.x;
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lds_hist[b] = 0;
+__global__ void __launch_bounds__(RC_THREADS) k_recode_hist(const uint32_t* __restrict__ scalars, MsmDims d,
+                                                            T* __restrict__ digits, uint32_t* __restrict__ hist_rows) {
+  extern __shared__ uint32_t lds_hist[];  // [W][nbc]
+  const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
+  const uint32_t ck = lo / d.ch;
+  const uint32_t nh = d.W * d.nbc;
+  for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) lds_hist[b] = 0;
   __syncthreads();
-  const T* dw = digits + (size_t)w * d.n;
-  const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += PT_THREADS) {
-    const uint32_t code = dw[i];
-    if (code != DigitCode<T>::ZERO) atomicAdd(&lds_hist[(code & DigitCode<T>::MAG) >> d.fb], 1u);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += RC_THREADS) {
+    uint32_t sw[8];
+    load_scalar(scalars, i, sw);
+    recode(sw, d, [&](uint32_t w, int32_t digit) {
+      uint32_t code = DigitCode<T>::ZERO;
+      if (digit != 0) {
+        const uint32_t mag = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
+        code = mag | (digit < 0 ? DigitCode<T>::SIGN : 0u);
+        atomicAdd(&lds_hist[w * d.nbc + (mag >> d.fb)], 1u);
+      }
+      digits[(size_t)w * d.n + i] = (T)code;
+    });
   }
   __syncthreads();
-  uint32_t* row = hist_rows + ((size_t)w * d.nch + ck) * d.nbc;
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) row[b] = lds_hist[b];
+  for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) {
+    const uint32_t v = lds_hist[b];
+    if (v) {
+      const uint32_t w = b / d.nbc, bin = b - w * d.nbc;
+      atomicAdd(&hist_rows[((size_t)w * d.nch + ck) * d.nbc + bin], v);
+    }
+  }
 }
 
 // Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
@@ -295,7 +340,6 @@ extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __
 // coarse bin.  The chunk is first counting-sorted by bin inside LDS, then streamed out so that
 // consecutive lanes write consecutive addresses of a slice (>= 64 entries per slice by
 // construction of ch): whole lines, one CU each.
-constexpr uint32_t PS_R = 16;  // digits per lane (ch <= PT_THREADS * PS_R)
 template <typename T>
 __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
                                                                         const uint32_t* __restrict__ hist_rows,
@@ -354,7 +398,10 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
 
 // Pass 3: one workgroup per coarse bin, counting sort by fine bucket (<= FS_MAXF per bin).  A bin
 // of at most FS_CAP entries is sorted inside LDS and streamed out coalesced; larger bins (skewed
-// scalars) loop over register tiles and scatter directly.
+// scalars) loop over register tiles and scatter directly.  Besides the sorted entry list it
+// writes the bucket boundaries the accumulation walks: bucket_start[key] (global position of
+// bucket `key`'s first entry; bucket_start[W*B] = bucket_start[W*B+1] = total) and
+// run_key[r] = the bucket holding position r*K (the first entry of accumulation run r).
 constexpr uint32_t FS_THREADS = 256;
 constexpr uint32_t FS_R = 24;
 constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS
@@ -363,12 +410,11 @@ constexpr uint32_t FS_MAXF = 2048;
 extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint32_t* __restrict__ part_entry,
                                                                      const uint16_t* __restrict__ part_fine,
                                                                      const uint32_t* __restrict__ bin_base, MsmDims d,
-                                                                     uint32_t* __restrict__ sorted_entry,
-                                                                     uint32_t* __restrict__ sorted_key,
-                                                                     uint32_t* __restrict__ bucket_count) {
+                                                                     uint32_t K, uint32_t* __restrict__ sorted_entry,
+                                                                     uint32_t* __restrict__ bucket_start,
+                                                                     uint32_t* __restrict__ run_key) {
   __shared__ uint32_t cnt[FS_MAXF];
   __shared__ uint32_t st_entry[FS_CAP];
-  __shared__ uint16_t st_fine[FS_CAP];
   const uint32_t bin = blockIdx.x;
   const uint32_t nf = 1u << d.fb;
   const uint32_t base = bin_base[bin];
@@ -391,9 +437,32 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
       if (fk[r] != 0xffffu) atomicAdd(&cnt[fk[r]], 1u);
   }
   __syncthreads();
-  for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) bucket_count[key0 + f] = cnt[f];
+  // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them
+  uint32_t my_cnt[FS_MAXF / FS_THREADS];
+#pragma unroll
+  for (uint32_t q = 0; q < FS_MAXF / FS_THREADS; q++) {
+    const uint32_t f = q * FS_THREADS + threadIdx.x;
+    my_cnt[q] = f < nf ? cnt[f] : 0u;
+  }
   __syncthreads();
   lds_excl_scan_wave0(cnt, nf);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t q = 0; q < FS_MAXF / FS_THREADS; q++) {
+    const uint32_t f = q * FS_THREADS + threadIdx.x;
+    if (f < nf) {
+      const uint32_t gs = base + cnt[f];
+      bucket_start[key0 + f] = gs;
+      if (my_cnt[q]) {
+        const uint32_t ge = gs + my_cnt[q];
+        for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
+      }
+    }
+  }
+  if (bin + 1 == gridDim.x && threadIdx.x == 0) {
+    bucket_start[d.W * d.B] = base + m;
+    bucket_start[d.W * d.B + 1] = base + m;
+  }
   __syncthreads();
   if (staged) {
 #pragma unroll
@@ -401,14 +470,10 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
       if (fk[r] != 0xffffu) {
         const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
         st_entry[p] = en[r];
-        st_fine[p] = (uint16_t)fk[r];
       }
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) {
-      sorted_entry[base + j] = st_entry[j];
-      sorted_key[base + j] = key0 + st_fine[j];
-    }
+    for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
     return;
   }
   for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
@@ -420,11 +485,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     }
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++) {
-      if (fk[r] != 0xffffu) {
-        const uint32_t pos = base + atomicAdd(&cnt[fk[r]], 1u);
-        sorted_entry[pos] = en[r];
-        sorted_key[pos] = key0 + fk[r];
-      }
+      if (fk[r] != 0xffffu) sorted_entry[base + atomicAdd(&cnt[fk[r]], 1u)] = en[r];
     }
   }
 }
@@ -487,14 +548,17 @@ __device__ __forceinline__ xyzt load_pt_lds(const uint32_t* src) {
 
 // Bucket accumulation over the sorted list.  Lane = run of K consecutive entries (perfect load
 // balance whatever the bucket sizes).  Inside a run, whole buckets are written straight to the
-// bucket table.  A bucket cut by run boundaries is joined without a second pass over HBM: every
-// run's leading piece (head) is staged in LDS, and after one barrier the run where the bucket
-// starts adds its trailing piece (tail) to the heads of the following runs of the same workgroup.
-// Only a chain leaving the workgroup goes to k_fixup (via a short list).
+// bucket table; bucket boundaries come from bucket_start (one load per bucket, issued a bucket
+// ahead), the run's first bucket from run_key.  A bucket cut by run boundaries is joined without
+// a second pass over HBM: every run's leading piece (head) is staged in LDS, and after one
+// barrier the run where the bucket starts adds its trailing piece (tail) to the heads of the
+// following runs of the same workgroup.  Only a chain leaving the workgroup goes to k_fixup (via
+// a short list).
 constexpr uint32_t ACC_THREADS = 256;
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
                                                                        const uint32_t* __restrict__ sorted_entry,
-                                                                       const uint32_t* __restrict__ sorted_key,
+                                                                       const uint32_t* __restrict__ bucket_start,
+                                                                       const uint32_t* __restrict__ run_key,
                                                                        const uint32_t* __restrict__ total_ptr, uint32_t K,
                                                                        uint32_t* __restrict__ buckets,
                                                                        uint32_t* __restrict__ run_head,
@@ -515,27 +579,33 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   bool has_tail = false;
   if (s < M) {
     const uint32_t e = min(s + K, M);
-    cur = sorted_key[s];
-    const bool started_before = s > 0 && sorted_key[s - 1] == cur;
+    cur = run_key[t];
+    const bool started_before = bucket_start[cur] < s;
+    uint32_t bend = bucket_start[cur + 1];   // end of bucket `cur`
+    uint32_t bnext = bucket_start[cur + 2];  // end of the bucket after it (prefetched)
     bool seg_first = true;
     for (uint32_t pos = s; pos < e; pos++) {
-      const uint32_t k = sorted_key[pos];
-      if (k != cur) {
+      if (pos == bend) {
         if (seg_first && started_before) {
           store_pt_lds(sh_head[lt], acc);
           sh_hkey[lt] = cur;
         } else {
           store_pt(buckets + (size_t)cur * PT_WORDS, acc);
         }
+        // advance to the next non-empty bucket
+        do {
+          cur++;
+          bend = bnext;
+          bnext = bucket_start[cur + 2];
+        } while (bend == pos);
         acc = pt_identity();
-        cur = k;
         seg_first = false;
       }
       const uint32_t ent = sorted_entry[pos];
       pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
       acc = pt_madd(acc, q);
     }
-    const bool cont = e < M && sorted_key[e] == cur;
+    const bool cont = bend > e;  // bucket `cur` continues into the next run
     if (seg_first && started_before) {  // the whole run belongs to a bucket begun earlier
       store_pt_lds(sh_head[lt], acc);
       sh_hkey[lt] = cur | (cont ? KEY_PASS : 0u);
@@ -614,7 +684,7 @@ extern "C" __global__ void __launch_bounds__(64) k_fixup(const uint32_t* __restr
 //   G_w = sum_c U_c + L * sum_c c T_c = R_{w,V} + sum_k 2^(lgL+k) R_{w,k},  R_{w,k} = sum_{c: bit k} T_c
 // ---------------------------------------------------------------------------------------------
 extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
-                                                                    const uint32_t* __restrict__ bucket_count, MsmDims d,
+                                                                    const uint32_t* __restrict__ bucket_start, MsmDims d,
                                                                     uint32_t L, uint32_t* __restrict__ out_U,
                                                                     uint32_t* __restrict__ out_T) {
   const uint32_t nchunks = d.B / L;
@@ -625,7 +695,7 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
   xyzt carry = pt_identity(), acc = pt_identity();
   bool carry_live = false, acc_live = false;
   for (int i = (int)L - 1; i >= 0; i--) {
-    if (bucket_count[key0 + i]) {
+    if (bucket_start[key0 + i + 1] != bucket_start[key0 + i]) {
       xyzt b = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
       carry = carry_live ? pt_add(carry, b) : b;
       carry_live = true;
@@ -639,23 +709,31 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
   store_pt(out_T + (size_t)g * PT_WORDS, carry);
 }
 
-// One workgroup per (window, term).  term 0: R_V = sum_c U_c; term 1+k: R_k = sum_{c: bit k of c} T_c.
-// Output: X, Y, T, Z in the host's Montgomery form (a * 2^256 mod p, 8 LE words each), so the
-// host Horner (hostfield.h) uses them without conversion.
+// One workgroup per (window, term).  Terms 0..nv-1: R_{V,v} = sum of U_c over the v-th slice of
+// chunks; term nv+k: R_k = sum_{c: bit k of c} T_c.  Every workgroup sums at most nchunks/2 points.
+// Output: X, Y, T, Z in the host's Montgomery form (a * 2^256 mod p, 8 LE words each), written
+// straight into coherent pinned host memory (no readback copy), so the host Horner
+// (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
+// entry count.
 constexpr int RED2_THREADS = 1024;
 extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(const uint32_t* __restrict__ in_U,
                                                                              const uint32_t* __restrict__ in_T,
-                                                                             uint32_t nchunks, uint32_t nterms,
-                                                                             uint32_t* __restrict__ out_std) {
+                                                                             uint32_t nchunks, uint32_t nv,
+                                                                             uint32_t nterms,
+                                                                             const uint32_t* __restrict__ err,
+                                                                             const uint32_t* __restrict__ total,
+                                                                             uint32_t* __restrict__ out_host) {
   __shared__ uint32_t sh[RED2_THREADS / 2][PT_WORDS];
   const uint32_t w = blockIdx.x / nterms, term = blockIdx.x % nterms;
-  const uint32_t* src = term == 0 ? in_U : in_T;
-  const uint32_t kbit = term - 1;
+  const bool vterm = term < nv;
+  const uint32_t* src = vterm ? in_U : in_T;
+  const uint32_t kbit = term - nv;
+  const uint32_t slice = nchunks / nv;
+  const uint32_t c0 = vterm ? term * slice : 0, c1 = vterm ? c0 + slice : nchunks;
   xyzt acc = pt_identity();
   bool live = false;
-  // the terms this thread owns: chunks c = tid, tid + 256, ... with (term==0 || bit k of c set)
-  for (uint32_t c = threadIdx.x; c < nchunks; c += RED2_THREADS) {
-    if (term != 0 && !((c >> kbit) & 1u)) continue;
+  for (uint32_t c = c0 + threadIdx.x; c < c1; c += RED2_THREADS) {
+    if (!vterm && !((c >> kbit) & 1u)) continue;
     xyzt p = load_pt(src + ((size_t)w * nchunks + c) * PT_WORDS);
     acc = live ? pt_add(acc, p) : p;
     live = true;
@@ -668,10 +746,21 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    uint32_t* o = out_std + (size_t)blockIdx.x * 32;
+    uint32_t* o = out_host + (size_t)blockIdx.x * 32;
     fe c4[4] = {fe_to_host_mont(acc.X), fe_to_host_mont(acc.Y), fe_to_host_mont(acc.T), fe_to_host_mont(acc.Z)};
+    uint32_t wd[8];
 #pragma unroll
-    for (int q = 0; q < 4; q++) fe_to_words_le(c4[q], o + 8 * q);
+    for (int q = 0; q < 4; q++) {
+      fe_to_words_le(c4[q], wd);
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[8 * q + k] = wd[k];
+    }
+    if (blockIdx.x == 0) {
+      const size_t tail = (size_t)gridDim.x * 32;
+      out_host[tail] = *err;
+      out_host[tail + 1] = *total;
+    }
+    __threadfence_system();
   }
 }
 

@@ -317,8 +317,11 @@ def gen_scalars(n: int, seed: int = XORSHIFT_SEED) -> np.ndarray:
     return o[: n * 8].reshape(n, 8)
 
 
-def set_profiling(enable: bool = True) -> None:
-    _check(load().msm_set_profiling(1 if enable else 0), "msm_set_profiling")
+def set_profiling(enable=True) -> None:
+    """0/False: off.  1/True: hipEvents between every phase (eager launches).  2: k_accumulate and
+    the device total only, keeping the captured-graph replay (what bench.py times)."""
+    mode = int(enable) if not isinstance(enable, bool) else (1 if enable else 0)
+    _check(load().msm_set_profiling(mode), "msm_set_profiling")
 
 
 def last_profile() -> dict:
