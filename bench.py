@@ -39,8 +39,8 @@ EXPECTED = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--run-length", type=int, default=0)
@@ -117,29 +117,47 @@ def main():
     window = args.window or None
     run_length = args.run_length or None
 
-    def step():
+    def steps(k):
+        """k complete MSMs of the workload; returns the last result.  On one GPU they go through
+        libmsm's pipelined entry (the device runs MSM i+1 while the host finishes MSM i's window
+        Horner); sharded, every step is one synchronous partial + all-gather + join."""
+        if k <= 0:
+            return None
         if world == 1:
-            return M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
-        return sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
+            out = M.compute_msm_many_device([d_pts] * k, [d_sc] * k, m, window_size=window,
+                                            run_length=run_length)
+            r = out[-1]
+            return (M.wire_to_int(r[:8]), M.wire_to_int(r[8:]))
+        res = None
+        for _ in range(k):
+            res = sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
+        return res
 
-    for _ in range(args.warmup):
-        res = step()
-    M.set_profiling(2)  # k_accumulate bracketed by hipEvents between graph replays
-    prof = []
+    res = steps(args.warmup)
+    M.set_profiling(2)  # k_accumulate bracketed by hipEvents between graph replays, every step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-        prof.append(M.last_profile())
+    res = steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # untimed: one eager pass with an event between every phase, for the breakdown
+    prof = M.last_profile()
+    M.set_profiling(False)
+    # untimed: single-MSM latency (no pipelining), and one eager pass with an event between
+    # every phase for the breakdown
+    lat = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        if world == 1:
+            M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
+        else:
+            sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
+        lat.append(time.perf_counter() - t1)
     M.set_profiling(1)
-    step()
+    M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
     phase_prof = M.last_profile()
     M.set_profiling(False)
     if world > 1:
@@ -154,8 +172,9 @@ def main():
             if not ok:
                 print(f"RESULT MISMATCH: got {res}, expected {EXPECTED[n]}", file=sys.stderr)
         ms = elapsed * 1e3 / args.steps
-        acc = float(np.mean([p["accumulate"] for p in prof]))
-        dev_total = float(np.mean([p["device_total"] for p in prof]))
+        nprof = max(1, int(prof["profiled"]))
+        acc = float(prof["accumulate_sum"]) / nprof  # mean k_accumulate duration over the timed MSMs
+        dev_total = float(prof["device_total_sum"]) / nprof
         algo_bytes = ALGO_BYTES_PER_POINT * m
         achieved = algo_bytes / (acc * 1e-3) / 1e9
         traffic = None
@@ -170,7 +189,7 @@ def main():
         phases = {k: round(float(phase_prof[k]), 4) for k in (
             "prepare_points", "recode_count", "coarse_scan", "coarse_scatter", "fine_sort", "accumulate",
             "fixup", "bucket_reduce_1", "bucket_reduce_2", "readback", "device_total", "host_tail")}
-        entries = int(prof[-1]["entries"])
+        entries = int(prof["entries"])
         # compute roofline: field multiplies per accumulation add = 7 (madd, ec.cuh)
         modmul_rate = entries * 7 / (acc * 1e-3) / 1e9
         line = {
@@ -187,8 +206,8 @@ def main():
             "dtype": "u32 (29-bit-limb Montgomery Fq, 253-bit)",
             "data": "synthetic: P_i=(i+1)G, xorshift64 scalars mod p (SURVEY.md §8c); result checked vs oracle-confirmed closed form",
             "config": {"workload": f"Edwards-BLS12 MSM, N=2^{int(np.log2(n))} points, point-sharded over {world} GPU(s)",
-                       "n_points": n, "window_bits": int(prof[-1]["window_bits"]), "windows": int(prof[-1]["windows"]),
-                       "run_length": int(prof[-1]["run_length"]), "parallelism": f"points{world}"},
+                       "n_points": n, "window_bits": int(prof["window_bits"]), "windows": int(prof["windows"]),
+                       "run_length": int(prof["run_length"]), "parallelism": f"points{world}"},
             "correct": ok,
             "roofline": {"bound": "hbm", "kernel": "k_accumulate", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -201,6 +220,9 @@ def main():
                                  "note": "peak = measured fe_mul throughput, tools/ubench/fmul_bench.hip"},
             "phases_ms": phases,
             "device_ms": round(dev_total, 4),
+            "latency_ms": round(float(np.median(lat)) * 1e3, 4),
+            "timing": "value = wall time of the K timed MSMs / K (pipelined: device runs MSM i+1 while the "
+                      "host finishes MSM i); latency_ms = one unpipelined MSM end to end (median of 5)",
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

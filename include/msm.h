@@ -49,6 +49,9 @@ typedef struct msm_profile_t {
   float host_tail;    /* host Horner + affine conversion (wall) */
   uint64_t entries;   /* nonzero digits sorted (= accumulation adds) */
   uint32_t window_bits, windows, run_length, chunk_len;
+  double accumulate_sum; /* sum of `accumulate` over every MSM profiled since msm_set_profiling */
+  double device_total_sum;
+  uint32_t profiled;     /* number of MSMs in those sums */
 } msm_profile_t;
 
 /* Library lifetime.  msm_init replaces the wasm init()/initThreadPool (submission.ts:89-93);
@@ -85,6 +88,13 @@ int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_
  * [count][n][8] scalars), all device-resident; results [count][16].  Prover-batch shape. */
 int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
                              const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
+
+/* `count` independent MSMs of n points each, inputs given by per-MSM device pointers; results
+ * [count][16].  Pipelined: MSM b+1 runs on the device while the host finishes MSM b (window
+ * Horner), so throughput exceeds 1 / latency.  msm_compute_batch_device is this with contiguous
+ * inputs. */
+int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
+                            size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
 
 /* point_add_affine (lib.rs:240-253): affine a + b -> affine, 16 words each. */
 int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]);

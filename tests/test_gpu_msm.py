@@ -225,3 +225,67 @@ def test_device_resident_entry():
     out = M.compute_msm_batch_device(torch.cat([dp, dp]), torch.cat([ds, ds]), n, 2)
     for r in out:
         assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == exp
+
+
+# --- skewed scalars: buckets that hold many accumulation runs (the reference's tree schedule,
+# gpu.ts:181-221, handles bucket-occupancy skew in O(log N) rounds; so must we) ---------------
+@pytest.mark.parametrize("n,run_length", [(20000, 1), (20000, 4), (1 << 16, 0), (1 << 18, 0)])
+def test_all_equal_scalars_giant_buckets(n, run_length):
+    import time
+
+    pts = O.gen_points(n, k0=11, step=1)
+    s = 0x0DEADBEEF1234567_89ABCDEF0FEDCBA9_8765432112345678_9ABCDEF011223344 % O.P
+    sc = O.ints_to_be_words([s] * n)
+    exp = O.closed_form_msm(range(11, 11 + n), [s] * n)
+    M.compute_msm_wire(pts, sc, run_length=run_length or None)  # warm (graph capture, allocation)
+    t0 = time.perf_counter()
+    got = M.compute_msm_wire(pts, sc, run_length=run_length or None)
+    dt = time.perf_counter() - t0
+    assert got == exp
+    # one bucket per window holds every point: must stay logarithmic, not O(runs) serial adds
+    assert dt < 0.05, f"skewed MSM took {dt * 1e3:.1f} ms"
+
+
+def test_few_distinct_scalars():
+    n = 50000
+    rng = np.random.default_rng(7)
+    vals = [int(v) for v in rng.integers(1, 2**62, size=3)]
+    ss = [vals[i % 3] * (2**190 + 12345) % O.P for i in range(n)]
+    pts = O.gen_points(n, k0=1000, step=3)
+    exp = O.closed_form_msm([1000 + 3 * i for i in range(n)], ss)
+    for K in (None, 2, 64):
+        assert M.compute_msm_wire(pts, O.ints_to_be_words(ss), run_length=K) == exp, K
+
+
+def test_small_scalars_sparse_windows():
+    # only the lowest window is populated; all higher windows are empty
+    n = 30000
+    ss = [(i * 7919) % 60000 for i in range(n)]
+    pts = O.gen_points(n, k0=5, step=2)
+    exp = O.closed_form_msm([5 + 2 * i for i in range(n)], ss)
+    assert M.compute_msm_wire(pts, O.ints_to_be_words(ss)) == exp
+    assert M.compute_msm_wire(pts, O.ints_to_be_words(ss), window_size=16) == exp
+
+
+def test_many_device_pipelined_distinct_inputs():
+    # msm_compute_many_device keeps two MSMs in flight (device runs b+1 while the host finishes b);
+    # every result must still be its own MSM's
+    torch = pytest.importorskip("torch")
+    n = 4096
+    cases = []
+    for j in range(5):
+        pts = O.gen_points(n, k0=3 + j, step=2 + j)
+        ss = O.xorshift_scalars(n, seed=100 + j)
+        exp = O.closed_form_msm([3 + j + (2 + j) * i for i in range(n)], ss)
+        cases.append((torch.from_numpy(pts.view(np.int32)).cuda(),
+                      torch.from_numpy(O.ints_to_be_words(ss).view(np.int32)).cuda(), exp))
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 3, 4, 2, 0, 4]
+    out = M.compute_msm_many_device([cases[i][0] for i in order], [cases[i][1] for i in order], n)
+    for r, i in zip(out, order):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == cases[i][2], i
+    # interleaved with single calls (slot rotation) and a different size (re-plan, re-capture)
+    assert M.compute_msm_device(cases[3][0], cases[3][1], n) == cases[3][2]
+    small = M.compute_msm_many_device([cases[1][0]], [cases[1][1]], 100)
+    assert (O.be_words_to_int(small[0][:8]), O.be_words_to_int(small[0][8:])) == \
+        O.closed_form_msm([4 + 3 * i for i in range(100)], O.xorshift_scalars(100, seed=101))

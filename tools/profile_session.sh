@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU tests, bench, and a rocprofv3 kernel-trace summary of a bench run.  Usage: bash tools/profile_session.sh <tag>
+set -u
+tag=${1:-r1}
+mkdir -p gpurun_out
+run() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -n 3 "gpurun_out/$name.txt" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout 600
+run bench 300 python bench.py
+export TMPDIR=/tmp
+run kstats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/kstats_$tag" -o run -- python bench.py --no-cpu-baseline

@@ -108,6 +108,46 @@ struct HostBuf {
   }
 };
 
+struct Plan {
+  MsmDims d;
+  uint32_t K;       // run length
+  uint32_t L;       // bucket-reduce chunk length
+  uint32_t lgL;
+  uint32_t nchunks; // B / L
+  uint32_t nv;      // V-slices: R_V = sum_c U_c is split into nv equal partial sums
+  uint32_t nterms;  // nv + log2(nchunks)
+  size_t Mmax;      // W * n upper bound on sorted entries
+  size_t runs_max;
+};
+
+// One in-flight MSM: its result buffer, its captured graphs and its events.  Two slots let
+// msm_compute_many_device keep MSM b+1 running on the GPU while the host finishes MSM b (window
+// Horner).
+struct Slot {
+  HostBuf h_out;  // k_bucket_reduce_2 writes the window terms, err and total here
+  void* h_out_dev = nullptr;
+  struct GraphKey {
+    size_t n;
+    uint32_t c, K;
+    int prof;
+    uint64_t gen;
+    bool operator==(const GraphKey& o) const {
+      return n == o.n && c == o.c && K == o.K && prof == o.prof && gen == o.gen;
+    }
+  } gkey{};
+  hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};  // whole MSM, or pre / - / post
+  // the two kernel nodes (in graph[0]) that take the MSM's input buffers: repointed per launch
+  hipGraphNode_t n_prep = nullptr, n_recode = nullptr;
+  hipKernelNodeParams p_prep{}, p_recode{};
+  const void *g_pts = nullptr, *g_sc = nullptr;  // inputs the instantiated graph currently reads
+  hipEvent_t ev_start = nullptr, ev_acc0 = nullptr, ev_acc1 = nullptr, ev_end = nullptr, ev_done = nullptr;
+  Plan pl{};
+  bool bracketed = false;
+};
+constexpr int NSLOT = 2;
+constexpr uint32_t PROF_EVERY = 4;
+
 struct DevCtx {
   int device = -1;
   int n_cu = 256;
@@ -115,25 +155,14 @@ struct DevCtx {
   std::mutex mu;
   Buf wire_points, wire_scalars, pts, err, digits, hist_rows, rel, colsum, bin_base;
   Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
-  Buf run_head, run_tail, head_key, tail_next, fix_list, red_U, red_T;
-  HostBuf h_out;         // k_bucket_reduce_2 writes the window terms, err and total here
-  void* h_out_dev = nullptr;
-  hipEvent_t ev[PH_COUNT] = {};
+  Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
+  Slot slot[NSLOT];
+  int next_slot = 0;
+  uint32_t prof_seq = 0;
+  hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
   int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate only (graph-friendly)
-  // The launch sequence of the last MSM shape, captured once into a HIP graph and replayed:
-  // one hipGraphLaunch instead of ~14 enqueues per MSM.
-  struct GraphKey {
-    const void *pts, *sc;
-    size_t n;
-    uint32_t c, K, L;
-    int prof;
-    uint64_t gen;
-    bool operator==(const GraphKey& o) const {
-      return pts == o.pts && sc == o.sc && n == o.n && c == o.c && K == o.K && L == o.L && prof == o.prof &&
-             gen == o.gen;
-    }
-  } gkey{};
-  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};  // whole MSM, or pre / - / post
+  // The launch sequence of each slot is captured once into HIP graphs and replayed: one
+  // hipGraphLaunch instead of ~16 enqueues per MSM.
   bool graphs_ok = true;
   msm_profile_t last{};
 };
@@ -179,6 +208,13 @@ int get_ctx(int device, DevCtx** out) {
       return MSM_ERR_HIP;
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
+    for (Slot& sl : c->slot) {
+      hipEventCreate(&sl.ev_start);
+      hipEventCreate(&sl.ev_acc0);
+      hipEventCreate(&sl.ev_acc1);
+      hipEventCreate(&sl.ev_end);
+      hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
       c->n_cu = prop.multiProcessorCount;
@@ -189,18 +225,6 @@ int get_ctx(int device, DevCtx** out) {
   *out = g_ctx[device];
   return MSM_OK;
 }
-
-struct Plan {
-  MsmDims d;
-  uint32_t K;       // run length
-  uint32_t L;       // bucket-reduce chunk length
-  uint32_t lgL;
-  uint32_t nchunks; // B / L
-  uint32_t nv;      // V-slices: R_V = sum_c U_c is split into nv equal partial sums
-  uint32_t nterms;  // nv + log2(nchunks)
-  size_t Mmax;      // W * n upper bound on sorted entries
-  size_t runs_max;
-};
 
 uint32_t ilog2(uint32_t v) {
   uint32_t r = 0;
@@ -234,10 +258,7 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
   while (kauto > 16 && (size_t)d.W * n / kauto < 262144) kauto >>= 1;
   pl->K = (o && o->run_length) ? o->run_length : kauto;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
-  uint32_t L = 8;
-  if (const char* e = getenv("MSM_RED_L")) L = (uint32_t)atoi(e);  // tuning override (power of 2)
-  if (L < 1 || (L & (L - 1))) L = 8;
-  pl->L = std::min<uint32_t>(L, d.B);
+  pl->L = RED_L;
   pl->lgL = ilog2(pl->L);
   pl->nchunks = d.B / pl->L;
   // every k_bucket_reduce_2 workgroup sums at most nchunks/2 points (the R_k terms' size)
@@ -253,6 +274,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   const MsmDims& d = pl.d;
   const size_t nb = (size_t)d.W * d.B;
   int rc;
+  const uint64_t gen0 = g_alloc_gen;
 #define ENS(buf, bytes) \
   if ((rc = c->buf.ensure(bytes)) != MSM_OK) return rc
   ENS(pts, (size_t)d.n * PRE_WORDS * 4);
@@ -268,18 +290,35 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
   ENS(bucket_start, (nb + 2) * 4);
   ENS(run_key, pl.runs_max * 4);
   ENS(buckets, nb * PT_WORDS * 4);
-  ENS(run_head, pl.runs_max * PT_WORDS * 4);
-  ENS(run_tail, pl.runs_max * PT_WORDS * 4);
-  ENS(head_key, pl.runs_max * 4);
-  ENS(tail_next, pl.runs_max * 4);
-  ENS(fix_list, (pl.runs_max / ACC_THREADS + 2) * 8 + 8);
+  const size_t nwg = pl.runs_max / ACC_THREADS + 2;
+  ENS(lead_val, nwg * PT_WORDS * 4);
+  ENS(lead_open, nwg * 4);
+  ENS(cross_key, nwg * 4);
+  ENS(lead_flag, 16);
+  ENS(skew_list, (nwg + 1) * 4);
+  ENS(g_head, pl.runs_max * PT_WORDS * 4);  // touched only by skewed workgroups
+  ENS(g_hkey, pl.runs_max * 4);
+  ENS(g_tkey, pl.runs_max * 4);
   ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
 #undef ENS
+  if (g_alloc_gen != gen0) {
+    // err, lead_flag and hist_rows are kept all-zero between MSMs by the kernels themselves
+    // (k_bucket_reduce_2 clears the flags, k_part_scatter the histogram rows it consumed), so a
+    // replayed graph needs no memset nodes; fresh allocations start that invariant here.
+    if (hipMemsetAsync(c->err.p, 0, c->err.cap, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->lead_flag.p, 0, c->lead_flag.cap, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->skew_list.p, 0, 4, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->hist_rows.p, 0, c->hist_rows.cap, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return MSM_ERR_HIP;
+  }
   const size_t hbytes = (size_t)d.W * pl.nterms * 32 * 4 + 64;
-  if (hbytes > c->h_out.cap || !c->h_out_dev) {
-    if ((rc = c->h_out.ensure(hbytes)) != MSM_OK) return rc;
-    if (hipHostGetDevicePointer(&c->h_out_dev, c->h_out.p, 0) != hipSuccess) return MSM_ERR_HIP;
+  for (Slot& sl : c->slot) {
+    if (hbytes > sl.h_out.cap || !sl.h_out_dev) {
+      if ((rc = sl.h_out.ensure(hbytes)) != MSM_OK) return rc;
+      if (hipHostGetDevicePointer(&sl.h_out_dev, sl.h_out.p, 0) != hipSuccess) return MSM_ERR_HIP;
+    }
   }
   return MSM_OK;
 }
@@ -290,9 +329,10 @@ inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((th
 // PART_PRE: memsets, point preparation and the sort; PART_ACC: bucket accumulation;
 // PART_POST: fixup and bucket reduction.
 constexpr int PART_PRE = 1, PART_ACC = 2, PART_POST = 4, PART_ALL = 7;
-int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s,
-                int parts = PART_ALL) {
+int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si,
+                hipStream_t s, int parts = PART_ALL) {
   const MsmDims& d = pl.d;
+  Slot& sl = c->slot[si];
   const bool prof = c->profiling == 1;
   auto mark = [&](int ph) {
     if (prof) hipEventRecord(c->ev[ph], s);
@@ -301,13 +341,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
   if (parts & PART_PRE) {
   mark(PH_START);
-  HIPCHECK(hipMemsetAsync(c->err.p, 0, 16, s));
-  HIPCHECK(hipMemsetAsync(c->fix_list.p, 0, 4, s));
   hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS)), dim3(PP_THREADS), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
                      c->err.as<uint32_t>());
   mark(PH_PREPARE);
   const size_t hist_lds = (size_t)d.W * d.nbc * 4;
-  HIPCHECK(hipMemsetAsync(c->hist_rows.p, 0, (size_t)d.nch * d.nbins * 4, s));
   const unsigned rc_grid = grid_for(d.n, RC_SPAN);
   if (d.c <= 16) {
     hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
@@ -340,23 +377,28 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   if (parts & PART_ACC) {
   hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, c->pts.as<uint32_t>(),
                      c->sorted_entry.as<uint32_t>(), c->bucket_start.as<uint32_t>(), c->run_key.as<uint32_t>(), total,
-                     pl.K, c->buckets.as<uint32_t>(),
-                     c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
-                     c->tail_next.as<uint32_t>(), c->fix_list.as<uint32_t>());
+                     pl.K, c->buckets.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->lead_open.as<uint32_t>(),
+                     c->cross_key.as<uint32_t>(), c->skew_list.as<uint32_t>(), c->g_head.as<uint32_t>(),
+                     c->g_hkey.as<uint32_t>(), c->g_tkey.as<uint32_t>());
   mark(PH_ACCUM);
   }
   if (parts & PART_POST) {
-  hipLaunchKernelGGL(k_fixup, dim3(grid_for(rgrid, 64)), dim3(64), 0, s, c->fix_list.as<uint32_t>(), total, pl.K,
-                     c->run_head.as<uint32_t>(), c->run_tail.as<uint32_t>(), c->head_key.as<uint32_t>(),
-                     c->tail_next.as<uint32_t>(), c->buckets.as<uint32_t>());
+  hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, c->skew_list.as<uint32_t>(), total, pl.K,
+                     c->g_head.as<uint32_t>(), c->g_hkey.as<uint32_t>(), c->g_tkey.as<uint32_t>(),
+                     c->buckets.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->lead_open.as<uint32_t>(),
+                     c->lead_flag.as<uint32_t>());
+  hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, c->lead_val.as<uint32_t>(),
+                     c->lead_open.as<uint32_t>(), c->lead_flag.as<uint32_t>(), total, pl.K);
   mark(PH_FIXUP);
   hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
-                     c->buckets.as<uint32_t>(), c->bucket_start.as<uint32_t>(), d, pl.L, c->red_U.as<uint32_t>(),
+                     c->buckets.as<uint32_t>(), c->bucket_start.as<uint32_t>(), d, pl.K,
+                     c->cross_key.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->red_U.as<uint32_t>(),
                      c->red_T.as<uint32_t>());
   mark(PH_RED1);
   hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, c->red_U.as<uint32_t>(),
-                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, c->err.as<uint32_t>(), total,
-                     reinterpret_cast<uint32_t*>(c->h_out_dev));
+                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, c->err.as<uint32_t>(),
+                     c->lead_flag.as<uint32_t>(), c->skew_list.as<uint32_t>(), total,
+                     reinterpret_cast<uint32_t*>(sl.h_out_dev));
   mark(PH_RED2);
   mark(PH_READBACK);
   }
@@ -436,19 +478,22 @@ bool graphs_enabled() {
   return on;
 }
 
-void drop_graphs(DevCtx* c) {
-  for (hipGraphExec_t& g : c->gexec)
-    if (g) {
-      hipGraphExecDestroy(g);
-      g = nullptr;
-    }
+void drop_graphs(Slot& sl) {
+  for (int i = 0; i < 3; i++) {
+    if (sl.gexec[i]) hipGraphExecDestroy(sl.gexec[i]);
+    if (sl.graph[i]) hipGraphDestroy(sl.graph[i]);
+    sl.gexec[i] = nullptr;
+    sl.graph[i] = nullptr;
+  }
+  sl.n_prep = sl.n_recode = nullptr;
+  sl.g_pts = sl.g_sc = nullptr;
 }
 
-int capture(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s, int parts,
-            hipGraphExec_t* out) {
+int capture(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si, hipStream_t s,
+            int parts, hipGraph_t* gout, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return MSM_ERR_HIP;
-  int rc = enqueue_msm(c, pl, d_points, d_scalars, s, parts);
+  int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts);
   hipError_t e = hipStreamEndCapture(s, &g);
   if (rc != MSM_OK || e != hipSuccess || !g) {
     if (g) hipGraphDestroy(g);
@@ -456,69 +501,198 @@ int capture(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t*
     return MSM_ERR_HIP;
   }
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
   if (e != hipSuccess) {
+    hipGraphDestroy(g);
     *out = nullptr;
     (void)hipGetLastError();
     return MSM_ERR_HIP;
   }
+  *gout = g;
   return MSM_OK;
 }
 
-// Enqueue one MSM.  The launch sequence of the last shape is captured into HIP graphs and
-// replayed (one hipGraphLaunch instead of ~14 enqueues).  Profiling mode 1 launches eagerly with
-// an event between every phase; mode 2 brackets an eager k_accumulate launch with events, between
-// two graphs (pre / post).  Captures only on the library's own stream (a caller's stream
-// may be capturing or in use).
-int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, hipStream_t s,
-               bool own_stream) {
-  const int prof = c->profiling;
-  const bool graphs = own_stream && c->graphs_ok && graphs_enabled() && prof != 1;
+// Find the input-reading kernel nodes of slot graph 0 so later launches can repoint them.
+int find_input_nodes(Slot& sl) {
+  size_t num = 0;
+  if (hipGraphGetNodes(sl.graph[0], nullptr, &num) != hipSuccess || num == 0) return MSM_ERR_HIP;
+  std::vector<hipGraphNode_t> nodes(num);
+  if (hipGraphGetNodes(sl.graph[0], nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
+  const void* f_prep = reinterpret_cast<const void*>(&k_prepare_points);
+  const void* f_rc16 = reinterpret_cast<const void*>(&k_recode_hist<uint16_t>);
+  const void* f_rc32 = reinterpret_cast<const void*>(&k_recode_hist<uint32_t>);
+  for (hipGraphNode_t nd : nodes) {
+    hipGraphNodeType ty;
+    if (hipGraphNodeGetType(nd, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess) continue;
+    if (kp.func == f_prep) {
+      sl.n_prep = nd;
+      sl.p_prep = kp;
+    } else if (kp.func == f_rc16 || kp.func == f_rc32) {
+      sl.n_recode = nd;
+      sl.p_recode = kp;
+    }
+  }
+  return sl.n_prep && sl.n_recode ? MSM_OK : MSM_ERR_HIP;
+}
+
+// Point the instantiated slot graph at new input buffers (kernel-node argument update, no
+// re-capture).
+int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points, const uint32_t* d_scalars) {
+  const MsmDims& d = pl.d;
+  const uint32_t* wire = d_points;
+  uint32_t* ptsb = c->pts.as<uint32_t>();
+  uint32_t n = d.n;
+  uint32_t* err = c->err.as<uint32_t>();
+  void* a_prep[] = {&wire, &ptsb, &n, &err};
+  hipKernelNodeParams kp = sl.p_prep;
+  kp.kernelParams = a_prep;
+  kp.extra = nullptr;
+  if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_prep, &kp) != hipSuccess) return MSM_ERR_HIP;
+  const uint32_t* scal = d_scalars;
+  MsmDims dd = d;
+  void* digits = c->digits.p;
+  uint32_t* hist = c->hist_rows.as<uint32_t>();
+  void* a_rc[] = {&scal, &dd, &digits, &hist};
+  hipKernelNodeParams kr = sl.p_recode;
+  kr.kernelParams = a_rc;
+  kr.extra = nullptr;
+  if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_recode, &kr) != hipSuccess) return MSM_ERR_HIP;
+  sl.g_pts = d_points;
+  sl.g_sc = d_scalars;
+  return MSM_OK;
+}
+
+// Enqueue one MSM in slot `si`.  The launch sequence of each slot is captured into HIP graphs and
+// replayed (one hipGraphLaunch instead of ~14 enqueues); new input buffers only repoint two
+// kernel nodes.  Profiling mode 1 launches eagerly with an event between every phase; mode 2
+// brackets an eager k_accumulate launch with events, between two graphs (pre / post).  Captures
+// only on the library's own stream (a caller's stream may be capturing or in use).
+int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si, hipStream_t s,
+               bool own_stream, bool bracket) {
+  Slot& sl = c->slot[si];
+  const int prof = bracket ? 2 : 0;
+  const bool graphs = own_stream && c->graphs_ok && graphs_enabled() && c->profiling != 1;
   if (graphs) {
-    DevCtx::GraphKey key{d_points, d_scalars, (size_t)pl.d.n, pl.d.c, pl.K, pl.L, prof, g_alloc_gen};
-    if (!(c->gexec[0] && key == c->gkey)) {
-      drop_graphs(c);
-      int rc = MSM_OK;
+    Slot::GraphKey key{(size_t)pl.d.n, pl.d.c, pl.K, prof, g_alloc_gen};
+    if (!(sl.gexec[0] && key == sl.gkey)) {
+      drop_graphs(sl);
+      int rc;
       if (prof == 2) {
-        rc = capture(c, pl, d_points, d_scalars, s, PART_PRE, &c->gexec[0]);
-        if (rc == MSM_OK) rc = capture(c, pl, d_points, d_scalars, s, PART_POST, &c->gexec[2]);
+        rc = capture(c, pl, d_points, d_scalars, si, s, PART_PRE, &sl.graph[0], &sl.gexec[0]);
+        if (rc == MSM_OK) rc = capture(c, pl, d_points, d_scalars, si, s, PART_POST, &sl.graph[2], &sl.gexec[2]);
       } else {
-        rc = capture(c, pl, d_points, d_scalars, s, PART_ALL, &c->gexec[0]);
+        rc = capture(c, pl, d_points, d_scalars, si, s, PART_ALL, &sl.graph[0], &sl.gexec[0]);
       }
+      if (rc == MSM_OK) rc = find_input_nodes(sl);
       if (rc != MSM_OK) {
-        drop_graphs(c);
+        drop_graphs(sl);
         c->graphs_ok = false;  // capture unsupported here: stay eager
       } else {
-        c->gkey = key;
+        sl.gkey = key;
+        sl.g_pts = d_points;
+        sl.g_sc = d_scalars;
       }
+    }
+    if (c->graphs_ok && (sl.g_pts != d_points || sl.g_sc != d_scalars) &&
+        repoint_inputs(c, pl, sl, d_points, d_scalars) != MSM_OK) {
+      drop_graphs(sl);
+      (void)hipGetLastError();
+      c->graphs_ok = false;
     }
   }
   const bool use_graphs = graphs && c->graphs_ok;
   if (prof == 2) {
-    HIPCHECK(hipEventRecord(c->ev[PH_START], s));
+    HIPCHECK(hipEventRecord(sl.ev_start, s));
     if (use_graphs) {
-      HIPCHECK(hipGraphLaunch(c->gexec[0], s));
-    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_PRE)) {
+      HIPCHECK(hipGraphLaunch(sl.gexec[0], s));
+    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_PRE)) {
       return rc;
     }
     // k_accumulate itself is launched eagerly between its two events: a graph launch there would
     // put the graph's own launch latency inside the measured bracket
-    HIPCHECK(hipEventRecord(c->ev[PH_FINE], s));
-    if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_ACC)) return rc;
-    HIPCHECK(hipEventRecord(c->ev[PH_ACCUM], s));
+    HIPCHECK(hipEventRecord(sl.ev_acc0, s));
+    if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC)) return rc;
+    HIPCHECK(hipEventRecord(sl.ev_acc1, s));
     if (use_graphs) {
-      HIPCHECK(hipGraphLaunch(c->gexec[2], s));
-    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, s, PART_POST)) {
+      HIPCHECK(hipGraphLaunch(sl.gexec[2], s));
+    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_POST)) {
       return rc;
     }
-    HIPCHECK(hipEventRecord(c->ev[PH_READBACK], s));
+    HIPCHECK(hipEventRecord(sl.ev_end, s));
     return MSM_OK;
   }
   if (use_graphs) {
-    HIPCHECK(hipGraphLaunch(c->gexec[0], s));
+    HIPCHECK(hipGraphLaunch(sl.gexec[0], s));
     return MSM_OK;
   }
-  return enqueue_msm(c, pl, d_points, d_scalars, s, PART_ALL);
+  return enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ALL);
+}
+
+// Start one MSM (device-resident inputs) in slot `si`; returns once it is enqueued.
+int submit_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si,
+               hipStream_t s) {
+  Slot& sl = c->slot[si];
+  sl.pl = pl;
+  // profiling mode 2 brackets k_accumulate with events on every PROF_EVERY-th MSM only (each
+  // bracket costs ~20 us of launch gaps); the mean over those is the reported duration
+  sl.bracketed = c->profiling == 2 && (c->prof_seq++ % PROF_EVERY) == 0;
+  int rc = launch_msm(c, pl, d_points, d_scalars, si, s, s == c->stream, sl.bracketed);
+  if (rc != MSM_OK) return rc;
+  HIPCHECK(hipEventRecord(sl.ev_done, s));
+  return MSM_OK;
+}
+
+// Wait for the MSM in slot `si` (spinning briefly: the result is usually due within a couple of
+// milliseconds, and a blocking wait adds a wake-up latency), then run its host tail.
+int finish_msm(DevCtx* c, int si, Pt* result) {
+  Slot& sl = c->slot[si];
+  const Plan& pl = sl.pl;
+  const auto spin_until = clk::now() + std::chrono::milliseconds(50);
+  hipError_t q;
+  while ((q = hipEventQuery(sl.ev_done)) == hipErrorNotReady && clk::now() < spin_until) _mm_pause();
+  if (q == hipErrorNotReady) q = hipEventSynchronize(sl.ev_done);
+  HIPCHECK(q);
+  const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(sl.h_out.p);
+  uint32_t err = h[outb / 4];
+  uint32_t total = h[outb / 4 + 1];
+  if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
+  if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
+  auto t0 = clk::now();
+  *result = horner_tail(pl, h);
+  auto t1 = clk::now();
+  if (c->profiling == 1 || (c->profiling == 2 && sl.bracketed)) {
+    float ms[PH_COUNT] = {};
+    msm_profile_t& P = c->last;
+    if (c->profiling == 1) {
+      for (int i = 1; i < PH_COUNT; i++) hipEventElapsedTime(&ms[i], c->ev[i - 1], c->ev[i]);
+      hipEventElapsedTime(&P.device_total, c->ev[PH_START], c->ev[PH_READBACK]);
+    } else {
+      hipEventElapsedTime(&ms[PH_ACCUM], sl.ev_acc0, sl.ev_acc1);
+      hipEventElapsedTime(&P.device_total, sl.ev_start, sl.ev_end);
+    }
+    P.prepare_points = ms[PH_PREPARE];
+    P.recode_count = ms[PH_RECODE];
+    P.coarse_scan = ms[PH_SCAN];
+    P.coarse_scatter = ms[PH_SCATTER];
+    P.fine_sort = ms[PH_FINE];
+    P.accumulate = ms[PH_ACCUM];
+    P.fixup = ms[PH_FIXUP];
+    P.bucket_reduce_1 = ms[PH_RED1];
+    P.bucket_reduce_2 = ms[PH_RED2];
+    P.readback = ms[PH_READBACK];
+    P.host_tail = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    P.entries = total;
+    P.window_bits = pl.d.c;
+    P.windows = pl.d.W;
+    P.run_length = pl.K;
+    P.chunk_len = pl.L;
+    P.accumulate_sum += P.accumulate;
+    P.device_total_sum += P.device_total;
+    P.profiled++;
+  }
+  return MSM_OK;
 }
 
 // Run one MSM with device inputs; result as a projective host point.
@@ -533,43 +707,41 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if (rc != MSM_OK) return rc;
   if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
   hipStream_t s = user_stream ? user_stream : c->stream;
-  if ((rc = launch_msm(c, pl, d_points, d_scalars, s, s == c->stream)) != MSM_OK) return rc;
-  HIPCHECK(hipStreamSynchronize(s));
-  const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
-  const uint32_t* h = reinterpret_cast<const uint32_t*>(c->h_out.p);
-  uint32_t err = h[outb / 4];
-  uint32_t total = h[outb / 4 + 1];
-  if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
-  if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
-  auto t0 = clk::now();
-  *result = horner_tail(pl, h);
-  auto t1 = clk::now();
-  if (c->profiling) {
-    float ms[PH_COUNT] = {};
-    msm_profile_t& P = c->last;
-    if (c->profiling == 1) {
-      for (int i = 1; i < PH_COUNT; i++) hipEventElapsedTime(&ms[i], c->ev[i - 1], c->ev[i]);
-    } else {
-      hipEventElapsedTime(&ms[PH_ACCUM], c->ev[PH_FINE], c->ev[PH_ACCUM]);
-    }
-    P.prepare_points = ms[PH_PREPARE];
-    P.recode_count = ms[PH_RECODE];
-    P.coarse_scan = ms[PH_SCAN];
-    P.coarse_scatter = ms[PH_SCATTER];
-    P.fine_sort = ms[PH_FINE];
-    P.accumulate = ms[PH_ACCUM];
-    P.fixup = ms[PH_FIXUP];
-    P.bucket_reduce_1 = ms[PH_RED1];
-    P.bucket_reduce_2 = ms[PH_RED2];
-    P.readback = ms[PH_READBACK];
-    hipEventElapsedTime(&P.device_total, c->ev[PH_START], c->ev[PH_READBACK]);
-    P.host_tail = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    P.entries = total;
-    P.window_bits = pl.d.c;
-    P.windows = pl.d.W;
-    P.run_length = pl.K;
-    P.chunk_len = pl.L;
+  const int si = c->next_slot;
+  c->next_slot = (si + 1) % NSLOT;
+  if ((rc = submit_msm(c, pl, d_points, d_scalars, si, s)) != MSM_OK) return rc;
+  return finish_msm(c, si, result);
+}
+
+// `count` MSMs of n points each, pipelined: MSM b+1 is enqueued before the host finishes MSM b,
+// so the host tail (window Horner) of one overlaps the device work of the next.
+int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* d_scalars, size_t n, size_t count,
+             const msm_opts* o, hipStream_t user_stream, uint32_t* out_xy_be) {
+  if (n == 0) {
+    for (size_t b = 0; b < count; b++) pt_to_be_affine(pt_identity(), out_xy_be + 16 * b);
+    return MSM_OK;
   }
+  Plan pl;
+  int rc = make_plan(n, o, c->n_cu, &pl);
+  if (rc != MSM_OK) return rc;
+  if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
+  hipStream_t s = user_stream ? user_stream : c->stream;
+  int first = c->next_slot;
+  for (size_t b = 0; b <= count; b++) {
+    if (b < count) {
+      if (!d_points[b] || !d_scalars[b]) return MSM_ERR_INVALID_ARG;
+      if ((rc = submit_msm(c, pl, d_points[b], d_scalars[b], (int)((first + b) % NSLOT), s)) != MSM_OK) return rc;
+    }
+    if (b >= 1) {
+      Pt r;
+      if ((rc = finish_msm(c, (int)((first + b - 1) % NSLOT), &r)) != MSM_OK) {
+        hipStreamSynchronize(s);
+        return rc;
+      }
+      pt_to_be_affine(r, out_xy_be + 16 * (b - 1));
+    }
+  }
+  c->next_slot = (int)((first + count) % NSLOT);
   return MSM_OK;
 }
 
@@ -628,12 +800,16 @@ void msm_shutdown(void) {
     hipStreamSynchronize(c->stream);
     Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->digits, &c->hist_rows, &c->rel, &c->colsum,
                    &c->bin_base, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->bucket_start,
-                   &c->run_key, &c->buckets, &c->run_head, &c->run_tail, &c->head_key, &c->tail_next, &c->fix_list,
+                   &c->run_key, &c->buckets, &c->lead_val, &c->lead_open, &c->cross_key, &c->lead_flag, &c->skew_list, &c->g_head, &c->g_hkey, &c->g_tkey,
                    &c->red_U, &c->red_T};
     for (Buf* b : bufs) b->release();
-    c->h_out.release();
-    c->h_out_dev = nullptr;
-    drop_graphs(c);
+    for (Slot& sl : c->slot) {
+      drop_graphs(sl);
+      sl.h_out.release();
+      sl.h_out_dev = nullptr;
+      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done})
+        if (e) hipEventDestroy(e);
+    }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
     hipSetDevice(prev);
@@ -734,15 +910,27 @@ int msm_compute_device_partial(const uint32_t* d_points_be, const uint32_t* d_sc
   return MSM_OK;
 }
 
+int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
+                            size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be) {
+  if (!out_xy_be || ((!d_points_be || !d_scalars_be) && count)) return MSM_ERR_INVALID_ARG;
+  if (count == 0) return MSM_OK;
+  DevCtx* c;
+  int rc = with_device(opts, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xy_be);
+}
+
 int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
                              const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be) {
   if (!out_xy_be || ((!d_points_be || !d_scalars_be) && n && count)) return MSM_ERR_INVALID_ARG;
+  std::vector<const uint32_t*> pp(count), ss(count);
   for (size_t b = 0; b < count; b++) {
-    int rc = msm_compute_device(d_points_be + b * n * 32, d_scalars_be + b * n * 8, n, opts, hip_stream,
-                                out_xy_be + 16 * b);
-    if (rc != MSM_OK) return rc;
+    pp[b] = d_points_be + b * n * 32;
+    ss[b] = d_scalars_be + b * n * 8;
   }
-  return MSM_OK;
+  return msm_compute_many_device(pp.data(), ss.data(), n, count, opts, hip_stream, out_xy_be);
 }
 
 int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]) {
@@ -802,7 +990,12 @@ int msm_set_profiling(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_profiling = enable < 0 ? 0 : enable > 2 ? 1 : enable;
   for (DevCtx* c : g_ctx)
-    if (c) c->profiling = g_profiling;
+    if (c) {
+      c->profiling = g_profiling;
+      c->last.accumulate_sum = c->last.device_total_sum = 0;
+      c->last.profiled = 0;
+      c->prof_seq = 0;
+    }
   return MSM_OK;
 }
 

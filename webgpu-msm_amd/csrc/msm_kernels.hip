@@ -14,7 +14,8 @@
 //   k_fine_sort        per coarse bin: LDS counting sort by bucket -> (entry, bucket key) lists
 //   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
 //                      written directly, buckets cut by run boundaries joined through LDS
-//   k_fixup            the few buckets whose run chain crosses a workgroup boundary
+//                      (segmented scan for long chains)
+//   k_lead_scan        chains bucket continuations that run through whole workgroups (skew only)
 //   k_bucket_reduce_1  per (window, chunk of L buckets): running sums -> U_c = sum (i+1) B, T_c = sum B
 //   k_bucket_reduce_2  per (window, term): plain sums R_{w,V} = sum_c U_c, R_{w,k} = sum_{c: bit k} T_c,
 //                      converted to canonical standard form for the host Horner
@@ -342,7 +343,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __
 // construction of ch): whole lines, one CU each.
 template <typename T>
 __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
-                                                                        const uint32_t* __restrict__ hist_rows,
+                                                                        uint32_t* __restrict__ hist_rows,
                                                                         const uint32_t* __restrict__ rel,
                                                                         const uint32_t* __restrict__ bin_base,
                                                                         uint32_t* __restrict__ part_entry,
@@ -358,6 +359,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
   const size_t row = ((size_t)w * d.nch + ck) * d.nbc;
   for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
     lcur[b] = hist_rows[row + b];
+    hist_rows[row + b] = 0;  // consumed: leaves the histogram zeroed for the next MSM's atomics
     gstart[b] = bin_base[w * d.nbc + b] + rel[row + b];
   }
   __syncthreads();
@@ -549,11 +551,21 @@ __device__ __forceinline__ xyzt load_pt_lds(const uint32_t* src) {
 // Bucket accumulation over the sorted list.  Lane = run of K consecutive entries (perfect load
 // balance whatever the bucket sizes).  Inside a run, whole buckets are written straight to the
 // bucket table; bucket boundaries come from bucket_start (one load per bucket, issued a bucket
-// ahead), the run's first bucket from run_key.  A bucket cut by run boundaries is joined without
-// a second pass over HBM: every run's leading piece (head) is staged in LDS, and after one
-// barrier the run where the bucket starts adds its trailing piece (tail) to the heads of the
-// following runs of the same workgroup.  Only a chain leaving the workgroup goes to k_fixup (via
-// a short list).
+// ahead), the run's first bucket from run_key.
+//
+// A bucket cut by run boundaries is joined without a second pass over HBM.  Every run's leading
+// piece (head: the entries of a bucket begun in an earlier run) is staged in LDS, flagged
+// "pass" when the whole run lies inside that bucket and the bucket continues.  After one barrier
+// the run where the bucket begins adds its trailing piece (tail) to the head of the next run.
+// A workgroup with a pass-through run (skewed scalars: a bucket holding several runs) instead
+// stages its heads and tails in HBM and leaves the joins to k_chain_join, which collapses the
+// chains with a logarithmic segmented scan; that keeps this kernel's register budget (and
+// occupancy) set by the main loop.
+//
+// A chain reaching the end of workgroup g continues in workgroup g+1's lane-0 chain ("lead"):
+// the tail owner stores its part in the bucket table and cross_key[g] names the bucket;
+// k_bucket_reduce_1 adds lead_val[g+1] to it, after k_lead_scan has chained leads that
+// themselves run through whole workgroups.
 constexpr uint32_t ACC_THREADS = 256;
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
                                                                        const uint32_t* __restrict__ sorted_entry,
@@ -561,22 +573,23 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
                                                                        const uint32_t* __restrict__ run_key,
                                                                        const uint32_t* __restrict__ total_ptr, uint32_t K,
                                                                        uint32_t* __restrict__ buckets,
-                                                                       uint32_t* __restrict__ run_head,
-                                                                       uint32_t* __restrict__ run_tail,
-                                                                       uint32_t* __restrict__ head_key,
-                                                                       uint32_t* __restrict__ tail_next,
-                                                                       uint32_t* __restrict__ fix_list) {
+                                                                       uint32_t* __restrict__ lead_val,
+                                                                       uint32_t* __restrict__ lead_open,
+                                                                       uint32_t* __restrict__ cross_key,
+                                                                       uint32_t* __restrict__ skew_list,
+                                                                       uint32_t* __restrict__ g_head,
+                                                                       uint32_t* __restrict__ g_hkey,
+                                                                       uint32_t* __restrict__ g_tkey) {
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
   __shared__ uint32_t sh_hkey[ACC_THREADS];
   const uint32_t M = *total_ptr;
-  const uint32_t nruns = (M + K - 1) / K;
   const uint32_t lt = threadIdx.x;
   const uint32_t t = blockIdx.x * ACC_THREADS + lt;
   const uint32_t s = t * K;
   sh_hkey[lt] = KEY_INVALID;
   xyzt acc = pt_identity();
   uint32_t cur = KEY_INVALID;
-  bool has_tail = false;
+  bool has_tail = false, cont = false;
   if (s < M) {
     const uint32_t e = min(s + K, M);
     cur = run_key[t];
@@ -605,7 +618,7 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
       pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
       acc = pt_madd(acc, q);
     }
-    const bool cont = bend > e;  // bucket `cur` continues into the next run
+    cont = bend > e;  // bucket `cur` continues into the next run
     if (seg_first && started_before) {  // the whole run belongs to a bucket begun earlier
       store_pt_lds(sh_head[lt], acc);
       sh_hkey[lt] = cur | (cont ? KEY_PASS : 0u);
@@ -615,67 +628,157 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
       store_pt(buckets + (size_t)cur * PT_WORDS, acc);
     }
   }
-  __syncthreads();
-  // Heads that a chain from the previous workgroup may need: runs preceded (within this WG) only
-  // by pass-through runs.  Normally just lane 0.
-  if (s < M && sh_hkey[lt] != KEY_INVALID) {
-    bool reachable = true;
-    for (uint32_t v = 0; v < lt; v++) {
-      const uint32_t hv = sh_hkey[v];
-      if (hv == KEY_INVALID || !(hv & KEY_PASS)) {
-        reachable = false;
-        break;
-      }
+  // the last live run of the workgroup says whether a bucket leaves the workgroup
+  const uint32_t nruns = (M + K - 1) / K;
+  const uint32_t last = min(ACC_THREADS, nruns - min(nruns, blockIdx.x * ACC_THREADS)) - 1;
+  if (lt == last) cross_key[blockIdx.x] = cont ? cur : KEY_INVALID;
+  const bool my_pass = sh_hkey[lt] != KEY_INVALID && (sh_hkey[lt] & KEY_PASS);
+  if (__syncthreads_or(my_pass)) {
+    // skewed workgroup: stage heads and tail pieces for k_chain_join
+    if (s < M) {
+      const uint32_t hk = sh_hkey[lt];
+      g_hkey[t] = hk;
+      if (hk != KEY_INVALID) store_pt(g_head + (size_t)t * PT_WORDS, load_pt_lds(sh_head[lt]));
+      g_tkey[t] = has_tail ? cur : KEY_INVALID;
+      if (has_tail) store_pt(buckets + (size_t)cur * PT_WORDS, acc);
     }
-    if (reachable) {
-      store_pt(run_head + (size_t)t * PT_WORDS, load_pt_lds(sh_head[lt]));
-      head_key[t] = sh_hkey[lt];
-    }
+    if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = blockIdx.x;
+    return;
+  }
+  // lane 0's head continues the previous workgroup's crossing bucket (never open here)
+  if (lt == 0) {
+    lead_open[blockIdx.x] = 0u;
+    if (s < M && sh_hkey[0] != KEY_INVALID) store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
   }
   if (has_tail) {
-    uint32_t lu = lt + 1;
-    bool done = false;
-    while (lu < ACC_THREADS && blockIdx.x * ACC_THREADS + lu < nruns) {
-      const uint32_t hk = sh_hkey[lu];
-      acc = pt_add(acc, load_pt_lds(sh_head[lu]));
-      if (!(hk & KEY_PASS)) {
-        done = true;
-        break;
-      }
-      lu++;
-    }
-    if (done) {
-      store_pt(buckets + (size_t)cur * PT_WORDS, acc);
-    } else {  // chain continues into the next workgroup's runs
-      store_pt(run_tail + (size_t)t * PT_WORDS, acc);
-      tail_next[t] = blockIdx.x * ACC_THREADS + lu;
-      const uint32_t slot = atomicAdd(&fix_list[0], 1u);
-      fix_list[1 + 2 * slot] = t;
-      fix_list[2 + 2 * slot] = cur;
-    }
+    // the bucket continues in run lt+1, whose head (not pass-through here) ends it
+    if (lt + 1 < ACC_THREADS) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
+    store_pt(buckets + (size_t)cur * PT_WORDS, acc);
   }
 }
 
-// Finishes the (rare) buckets whose run chain crosses a workgroup boundary: tail piece + heads of
-// the next workgroup's leading runs (pass-through runs continue the chain).
-extern "C" __global__ void __launch_bounds__(64) k_fixup(const uint32_t* __restrict__ fix_list,
-                                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
-                                                         const uint32_t* __restrict__ run_head,
-                                                         const uint32_t* __restrict__ run_tail,
-                                                         const uint32_t* __restrict__ head_key,
-                                                         const uint32_t* __restrict__ tail_next,
-                                                         uint32_t* __restrict__ buckets) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= fix_list[0]) return;
-  const uint32_t nruns = (*total_ptr + K - 1) / K;
-  const uint32_t t = fix_list[1 + 2 * i], key = fix_list[2 + 2 * i];
-  xyzt acc = load_pt(run_tail + (size_t)t * PT_WORDS);
-  for (uint32_t u = tail_next[t]; u < nruns; u++) {
-    acc = pt_add(acc, load_pt(run_head + (size_t)u * PT_WORDS));
-    const uint32_t hk = head_key[u];
-    if (!(hk & KEY_PASS)) break;
+// Joins for workgroups that k_accumulate found to hold a pass-through run (skewed scalars).
+// Segmented suffix scan over the workgroup's heads by pointer jumping: after it, head r holds
+// h_r + h_{r+1} + ... to the end of r's chain (or the workgroup's end), and its pass bit says
+// whether the chain leaves the workgroup; log2(256) steps of one point add.  Then every tail
+// owner adds the chain that follows it, and lane 0 publishes the workgroup's lead.
+constexpr uint32_t CJ_GRID = 256;  // k_chain_join workgroups (they loop over the skewed list)
+extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uint32_t* __restrict__ skew_list,
+                                                                       const uint32_t* __restrict__ total_ptr,
+                                                                       uint32_t K,
+                                                                       const uint32_t* __restrict__ g_head,
+                                                                       const uint32_t* __restrict__ g_hkey,
+                                                                       const uint32_t* __restrict__ g_tkey,
+                                                                       uint32_t* __restrict__ buckets,
+                                                                       uint32_t* __restrict__ lead_val,
+                                                                       uint32_t* __restrict__ lead_open,
+                                                                       uint32_t* __restrict__ lead_flag) {
+  const uint32_t nskew = skew_list[0];
+  if (blockIdx.x >= nskew) return;
+  const uint32_t M = *total_ptr;
+  const uint32_t nruns = (M + K - 1) / K;
+  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
+  __shared__ uint32_t sh_hkey[ACC_THREADS];
+  const uint32_t lt = threadIdx.x;
+  for (uint32_t li = blockIdx.x; li < nskew; li += gridDim.x) {
+  const uint32_t wg = skew_list[1 + li];
+  const uint32_t t = wg * ACC_THREADS + lt;
+  const bool live = t < nruns;
+  const uint32_t hk = live ? g_hkey[t] : KEY_INVALID;
+  sh_hkey[lt] = hk;
+  xyzt v = pt_identity();
+  if (hk != KEY_INVALID) {
+    v = load_pt(g_head + (size_t)t * PT_WORDS);
+    store_pt_lds(sh_head[lt], v);
   }
-  store_pt(buckets + (size_t)key * PT_WORDS, acc);
+  bool open = hk != KEY_INVALID && (hk & KEY_PASS);
+  __syncthreads();
+  for (uint32_t d = 1; d < ACC_THREADS; d <<= 1) {
+    const bool take = open && lt + d < ACC_THREADS;
+    xyzt nv;
+    bool nopen = false;
+    if (take) {
+      nv = load_pt_lds(sh_head[lt + d]);
+      nopen = (sh_hkey[lt + d] & KEY_PASS) != 0;
+    }
+    __syncthreads();
+    if (take) {
+      v = pt_add(v, nv);
+      open = nopen;
+      store_pt_lds(sh_head[lt], v);
+      sh_hkey[lt] = (sh_hkey[lt] & ~KEY_PASS) | (open ? KEY_PASS : 0u);
+    }
+    __syncthreads();
+  }
+  if (lt == 0) {
+    const uint32_t h0 = sh_hkey[0];
+    const bool has_head = h0 != KEY_INVALID;
+    const bool lopen = has_head && (h0 & KEY_PASS);
+    if (has_head) store_pt(lead_val + (size_t)wg * PT_WORDS, load_pt_lds(sh_head[0]));
+    lead_open[wg] = lopen ? 1u : 0u;
+    if (lopen) atomicOr(lead_flag, 1u);
+  }
+  const uint32_t tk = live ? g_tkey[t] : KEY_INVALID;
+  if (tk != KEY_INVALID) {
+    xyzt acc = load_pt(buckets + (size_t)tk * PT_WORDS);
+    if (lt + 1 < ACC_THREADS) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
+    store_pt(buckets + (size_t)tk * PT_WORDS, acc);
+  }
+  __syncthreads();  // LDS reused by the next listed workgroup
+  }
+}
+
+// Chains leads that run through whole workgroups (a bucket spanning three or more workgroups):
+// segmented suffix scan lead_val[g] <- lead_val[g] + lead_val[g+1] + ... while lead_open.  One
+// workgroup walks the leads from the end in tiles of LS_THREADS; a no-op unless k_accumulate saw
+// an open lead.
+constexpr uint32_t LS_THREADS = 512;
+extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* __restrict__ lead_val,
+                                                                     const uint32_t* __restrict__ lead_open,
+                                                                     const uint32_t* __restrict__ lead_flag,
+                                                                     const uint32_t* __restrict__ total_ptr,
+                                                                     uint32_t K) {
+  if (*lead_flag == 0) return;
+  __shared__ uint32_t sv[LS_THREADS][PT_WORDS];
+  __shared__ uint32_t so[LS_THREADS];
+  const uint32_t M = *total_ptr;
+  const uint32_t nruns = (M + K - 1) / K;
+  const uint32_t nwg = (nruns + ACC_THREADS - 1) / ACC_THREADS;
+  const uint32_t i = threadIdx.x;
+  const uint32_t ntiles = (nwg + LS_THREADS - 1) / LS_THREADS;
+  for (int tile = (int)ntiles - 1; tile >= 0; tile--) {
+    const uint32_t g = (uint32_t)tile * LS_THREADS + i;
+    // every lead an open lead can reach is valid (an open chain enters the next workgroup's
+    // lane 0); other slots may hold stale data and are never absorbed
+    bool open = g < nwg && lead_open[g] != 0;
+    xyzt v = g < nwg ? load_pt(lead_val + (size_t)g * PT_WORDS) : pt_identity();
+    store_pt_lds(sv[i], v);
+    so[i] = open ? 1u : 0u;
+    __syncthreads();
+    for (uint32_t d = 1; d < LS_THREADS; d <<= 1) {
+      const bool take = open && i + d < LS_THREADS && g + d < nwg;
+      xyzt nv;
+      bool nopen = false;
+      if (take) {
+        nv = load_pt_lds(sv[i + d]);
+        nopen = so[i + d] != 0;
+      }
+      __syncthreads();
+      if (take) {
+        v = pt_add(v, nv);
+        open = nopen;
+        store_pt_lds(sv[i], v);
+        so[i] = open ? 1u : 0u;
+      }
+      __syncthreads();
+    }
+    // still open at the tile's end: absorb the (final) value of the next tile's first lead
+    const uint32_t gn = (uint32_t)(tile + 1) * LS_THREADS;
+    if (open && gn < nwg) v = pt_add(v, load_pt(lead_val + (size_t)gn * PT_WORDS));
+    __syncthreads();
+    if (g < nwg && lead_open[g] != 0) store_pt(lead_val + (size_t)g * PT_WORDS, v);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -683,20 +786,48 @@ extern "C" __global__ void __launch_bounds__(64) k_fixup(const uint32_t* __restr
 //   chunk c (L buckets): U_c = sum_i (i+1) B_{cL+i}, T_c = sum_i B_{cL+i}   (running sums)
 //   G_w = sum_c U_c + L * sum_c c T_c = R_{w,V} + sum_k 2^(lgL+k) R_{w,k},  R_{w,k} = sum_{c: bit k} T_c
 // ---------------------------------------------------------------------------------------------
+constexpr uint32_t RED_L = 8;  // buckets per k_bucket_reduce_1 lane (c >= 4 gives B >= 8)
 extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
                                                                     const uint32_t* __restrict__ bucket_start, MsmDims d,
-                                                                    uint32_t L, uint32_t* __restrict__ out_U,
+                                                                    uint32_t K,
+                                                                    const uint32_t* __restrict__ cross_key,
+                                                                    const uint32_t* __restrict__ lead_val,
+                                                                    uint32_t* __restrict__ out_U,
                                                                     uint32_t* __restrict__ out_T) {
-  const uint32_t nchunks = d.B / L;
+  const uint32_t nchunks = d.B / RED_L;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= d.W * nchunks) return;
   const uint32_t w = g / nchunks, c = g % nchunks;
-  const uint32_t key0 = w * d.B + c * L;
+  const uint32_t key0 = w * d.B + c * RED_L;
+  // bucket metadata up front (independent loads): which buckets are non-empty, and which left
+  // their accumulation workgroup and need the continuation from lead_val
+  uint32_t bs[RED_L + 1];
+#pragma unroll
+  for (uint32_t i = 0; i <= RED_L; i++) bs[i] = bucket_start[key0 + i];
+  uint32_t live = 0, cross = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < RED_L; i++) {
+    if (bs[i + 1] != bs[i]) {
+      live |= 1u << i;
+      if (cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
+    }
+  }
   xyzt carry = pt_identity(), acc = pt_identity();
   bool carry_live = false, acc_live = false;
-  for (int i = (int)L - 1; i >= 0; i--) {
-    if (bucket_start[key0 + i + 1] != bucket_start[key0 + i]) {
-      xyzt b = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
+  // running sums from the top bucket down; the next live bucket's load is issued before the
+  // current bucket's adds
+  int i = 31 - __builtin_clz(live | 1u);
+  xyzt nb = (live >> i) & 1u ? load_pt(buckets + (size_t)(key0 + i) * PT_WORDS) : pt_identity();
+#pragma unroll 1
+  for (; i >= 0; i--) {
+    if ((live >> i) & 1u) {
+      xyzt b = nb;
+      const uint32_t below = live & ((1u << i) - 1u);
+      if (below) nb = load_pt(buckets + (size_t)(key0 + 31 - __builtin_clz(below)) * PT_WORDS);
+      if ((cross >> i) & 1u) {  // rare: reload the bucket's start rather than index bs[] dynamically
+        const uint32_t g0 = (bucket_start[key0 + i] / K) / ACC_THREADS;
+        b = pt_add(b, load_pt(lead_val + (size_t)(g0 + 1) * PT_WORDS));
+      }
       carry = carry_live ? pt_add(carry, b) : b;
       carry_live = true;
     }
@@ -720,7 +851,9 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
                                                                              const uint32_t* __restrict__ in_T,
                                                                              uint32_t nchunks, uint32_t nv,
                                                                              uint32_t nterms,
-                                                                             const uint32_t* __restrict__ err,
+                                                                             uint32_t* __restrict__ err,
+                                                                             uint32_t* __restrict__ lead_flag,
+                                                                             uint32_t* __restrict__ skew_list,
                                                                              const uint32_t* __restrict__ total,
                                                                              uint32_t* __restrict__ out_host) {
   __shared__ uint32_t sh[RED2_THREADS / 2][PT_WORDS];
@@ -759,6 +892,9 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
       const size_t tail = (size_t)gridDim.x * 32;
       out_host[tail] = *err;
       out_host[tail + 1] = *total;
+      *err = 0;  // flags start the next MSM cleared (no memset node in the graph)
+      *lead_flag = 0;
+      skew_list[0] = 0;
     }
     __threadfence_system();
   }
