@@ -632,11 +632,17 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   const uint32_t nruns = (M + K - 1) / K;
   const uint32_t last = min(ACC_THREADS, nruns - min(nruns, blockIdx.x * ACC_THREADS)) - 1;
   if (lt == last) cross_key[blockIdx.x] = cont ? cur : KEY_INVALID;
-  const bool my_pass = sh_hkey[lt] != KEY_INVALID && (sh_hkey[lt] & KEY_PASS);
-  if (__syncthreads_or(my_pass)) {
+  __syncthreads();
+  // Chains of heads: a run whose head is "pass" continues into the next run.  Runs of two or more
+  // pass heads in a row (dense buckets: skewed scalars, or the sparse top window) are deferred
+  // to k_chain_join's logarithmic scan; otherwise every chain has at most one pass head and is
+  // joined right here with at most two adds.
+  const uint32_t hk = sh_hkey[lt];
+  const bool my_pass = hk != KEY_INVALID && (hk & KEY_PASS);
+  const bool nxt_pass = lt < last && (sh_hkey[lt + 1] & KEY_PASS) && sh_hkey[lt + 1] != KEY_INVALID;
+  if (__syncthreads_or((my_pass && nxt_pass) || (lt == 0 && my_pass))) {
     // skewed workgroup: stage heads and tail pieces for k_chain_join
     if (s < M) {
-      const uint32_t hk = sh_hkey[lt];
       g_hkey[t] = hk;
       if (hk != KEY_INVALID) store_pt(g_head + (size_t)t * PT_WORDS, load_pt_lds(sh_head[lt]));
       g_tkey[t] = has_tail ? cur : KEY_INVALID;
@@ -645,14 +651,18 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
     if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = blockIdx.x;
     return;
   }
-  // lane 0's head continues the previous workgroup's crossing bucket (never open here)
+  // lane 0's head (never pass here) is the end of the previous workgroup's crossing bucket
   if (lt == 0) {
     lead_open[blockIdx.x] = 0u;
-    if (s < M && sh_hkey[0] != KEY_INVALID) store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
+    if (s < M && hk != KEY_INVALID) store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
   }
   if (has_tail) {
-    // the bucket continues in run lt+1, whose head (not pass-through here) ends it
-    if (lt + 1 < ACC_THREADS) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
+    // the bucket continues in run lt+1 (and lt+2 if lt+1 is pass-through), unless it leaves the
+    // workgroup: then k_bucket_reduce_1 adds the next workgroup's lead (cross_key).  (Two
+    // straight-line adds: the same in a loop costs ~50 more VGPRs and occupancy.)
+    const uint32_t nwalk = lt < last ? 1u + ((nxt_pass && lt + 1 < last) ? 1u : 0u) : 0u;
+    if (nwalk) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
+    if (nwalk > 1) acc = pt_add(acc, load_pt_lds(sh_head[lt + 2]));
     store_pt(buckets + (size_t)cur * PT_WORDS, acc);
   }
 }
