@@ -7,10 +7,18 @@ A "step" is one complete MSM of the whole N-point workload (config: BASELINE.jso
 "2^20-point MSM on 1xMI355X, auto-tuned window").  Inputs are synthetic and already resident in
 HBM when the timed region starts: P_i = (i+1) G (G = the benchmark page's point,
 src/ui/AllBenchmarks.tsx:111-119), scalars = xorshift64 words mod p (SURVEY.md §8c spec), so
-the result is checked against the oracle-confirmed closed-form value.  With N > 1 ranks every
-rank takes a contiguous 1/N of the points (no data-path collective), computes its partial
-point, and the partials are all-gathered over RCCL (torch.distributed "nccl") and added on rank
-0: strong scaling of one MSM.  Rank 0 prints ONE JSON line.
+the result is checked against the oracle-confirmed closed-form value.
+
+The K timed steps go through libmsm's pipelined entry (msm_compute_many_device): two slots, each
+with its own stream and workspace, so step i+1 runs on the device while the host finishes step
+i's window Horner.  `value` = wall time of the K steps / K (whole-job throughput); `latency_ms`
+is one unpipelined MSM end to end.
+
+With N > 1 ranks every rank takes a contiguous 1/N of the points (no data-path collective),
+computes its K partial points (pipelined the same way), the K x 128 B partials are all-gathered
+over RCCL (torch.distributed "nccl") in one collective and rank 0 adds each step's N partials:
+strong scaling of the MSM (BASELINE configs[3]).  Rank 0 prints ONE JSON line.
+MSM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU.
 """
 import argparse
 import json
@@ -96,13 +104,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    backend = os.environ.get("MSM_DIST_BACKEND", "nccl")
+    local_dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    gather_dev = dev if backend != "gloo" else None
 
-    from msm_amd.dist import shard_range, sharded_msm_device
+    from msm_amd.dist import shard_range, sharded_msm_device, sharded_msm_many_device
 
     n = args.n
     lo, hi = shard_range(n, rank, world)
@@ -128,10 +142,9 @@ def main():
                                             run_length=run_length)
             r = out[-1]
             return (M.wire_to_int(r[:8]), M.wire_to_int(r[8:]))
-        res = None
-        for _ in range(k):
-            res = sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
-        return res
+        # every rank pipelines its K partials; one all_gather carries all K x 128 B per rank
+        out = sharded_msm_many_device([d_pts] * k, [d_sc] * k, m, rank, device=gather_dev, window_size=window)
+        return out[-1] if out is not None else None
 
     res = steps(args.warmup)
     M.set_profiling(2)  # k_accumulate bracketed by hipEvents between graph replays, every step
@@ -154,14 +167,14 @@ def main():
         if world == 1:
             M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
         else:
-            sharded_msm_device(d_pts, d_sc, m, rank, device=dev, window_size=window)
+            sharded_msm_device(d_pts, d_sc, m, rank, device=gather_dev, window_size=window)
         lat.append(time.perf_counter() - t1)
     M.set_profiling(1)
     M.compute_msm_device(d_pts, d_sc, m, window_size=window, run_length=run_length)
     phase_prof = M.last_profile()
     M.set_profiling(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=gather_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 

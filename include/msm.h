@@ -95,6 +95,11 @@ int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scal
  * inputs. */
 int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
                             size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
+/* Same, each result as a projective X|Y|T|Z partial ([count][32] words) for a later
+ * msm_combine_partials: the pipelined shard entry of a multi-GPU batch. */
+int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be,
+                                    size_t n, size_t count, const msm_opts* opts, void* hip_stream,
+                                    uint32_t* out_xyzt_be);
 
 /* point_add_affine (lib.rs:240-253): affine a + b -> affine, 16 words each. */
 int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]);

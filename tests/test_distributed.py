@@ -61,3 +61,46 @@ def test_sharded_join_gloo(world, n):
         assert p.exitcode == 0
     assert res == O.closed_form_msm(range(1, n + 1), O.xorshift_scalars(n))
     assert sum(b - a for a, b in (shard_range(n, r, world) for r in range(world))) == n
+
+
+def _batch_worker(rank, world, port, n, k, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "webgpu-msm_amd")]
+    import torch.distributed as dist
+    from msm_amd.dist import shard_range, gather_partials, combine_batch_on_root
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(n, rank, world)
+    parts = np.zeros((k, 32), np.uint32)
+    for b in range(k):  # K different MSMs: scalar seeds differ per MSM
+        ss = O.xorshift_scalars(n, seed=1000 + b)[lo:hi]
+        x, y = O.closed_form_msm(range(lo + 1, hi + 1), ss) if hi > lo else O.IDENTITY
+        z = 2 + rank + b
+        for j, v in enumerate((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)):
+            parts[b, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
+    res = combine_batch_on_root(gather_partials(parts), rank)
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,k", [(2, 500, 3), (3, 100, 2)])
+def test_sharded_batch_join_gloo(world, n, k):
+    # the pipelined multi-GPU bench path: K partials per rank, one all_gather, K joins on rank 0
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, n, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [O.closed_form_msm(range(1, n + 1), O.xorshift_scalars(n, seed=1000 + b)) for b in range(k)]

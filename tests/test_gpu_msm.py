@@ -60,7 +60,7 @@ def test_point_ops_vs_oracle(golden):
         qs.append(O.point_from_x(int(x)))
     P_ = np.concatenate([_le_words([p[0] for p in ps]), _le_words([p[1] for p in ps])], axis=1)
     Q_ = np.concatenate([_le_words([q[0] for q in qs]), _le_words([q[1] for q in qs])], axis=1)
-    for op in (0, 1, 2):
+    for op in (0, 1, 2, 3):  # 3: quad-cooperative add (pt_add_quad)
         out = M._test_point_op(op, P_, Q_)
         for i in range(len(ps)):
             X, Y, T, Z = (_from_le(out[i, 8 * j: 8 * j + 8]) for j in range(4))

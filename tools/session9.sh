@@ -1,0 +1,16 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+run() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -n 3 "gpurun_out/$name.txt" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout 600
+run bench 300 python bench.py
+MSM_DIST_BACKEND=gloo run bench2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline

@@ -113,4 +113,37 @@ __device__ __forceinline__ xyzt pt_sel(bool c, const xyzt& a, const xyzt& b) {
   return r;
 }
 
+// ---- quad-cooperative addition (latency-bound reductions) -------------------------------------
+// Lane q = lane & 3 of each group of 4 lanes holds coordinate q (0 X, 1 Y, 2 T, 3 Z) of P in `p`
+// and of Q in `r`; every lane gets its coordinate of P + Q.  Same add-2008-hwcd-3 formula as
+// pt_add, but its 9 multiplies run as 3 rounds of one multiply per lane (A | B | T1T2 | Z1Z2, then
+// C = 2d T1T2, then EF | GH | EH | FG), operands exchanged with DPP quad permutes.  Three
+// multiply latencies instead of nine: for reduction trees whose levels are too narrow to fill
+// the machine.
+template <int K>
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], K * 0x55, 0xF, 0xF, false);
+  return r;
+}
+__device__ __forceinline__ fe pt_add_quad(const fe& p, const fe& r) {
+  const uint32_t q = threadIdx.x & 3;
+  const fe X1 = fe_quad_bcast<0>(p), Y1 = fe_quad_bcast<1>(p);
+  const fe X2 = fe_quad_bcast<0>(r), Y2 = fe_quad_bcast<1>(r);
+  const fe s1 = fe_sub_u(Y1, X1), a1 = fe_add(Y1, X1);  // U, S
+  const fe s2 = fe_sub(Y2, X2), a2 = fe_add(Y2, X2);    // N, S
+  fe a = fe_sel(q == 0, fe_sel(q == 1, p, a1), s1);
+  fe b = fe_sel(q == 0, fe_sel(q == 1, r, a2), s2);
+  const fe m = fe_mul(a, b);  // lane 0: A, 1: B, 2: T1 T2, 3: Z1 Z2
+  const fe m2 = fe_mul(m, fe_sel(q == 2, fe_one(), fe_const(K2D29)));  // lane 2: C = 2d T1 T2
+  const fe A = fe_quad_bcast<0>(m2), B = fe_quad_bcast<1>(m2);
+  const fe C = fe_quad_bcast<2>(m2), D0 = fe_quad_bcast<3>(m2);
+  const fe D = fe_add(D0, D0);
+  const fe E = fe_sub_u(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  const fe a3 = fe_sel(q == 0 || q == 2, fe_sel(q == 1, F, G), E);  // E F | G H | E H | F G
+  const fe b3 = fe_sel(q == 0, fe_sel(q == 3, H, G), F);
+  return fe_mul(a3, b3);
+}
+
 }  // namespace msm

@@ -120,10 +120,26 @@ struct Plan {
   size_t runs_max;
 };
 
-// One in-flight MSM: its result buffer, its captured graphs and its events.  Two slots let
-// msm_compute_many_device keep MSM b+1 running on the GPU while the host finishes MSM b (window
-// Horner).
+// Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
+struct Workspace {
+  Buf pts, err, digits, hist_rows, rel, colsum, bin_base;
+  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
+  Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
+  void release() {
+    Buf* bufs[] = {&pts, &err, &digits, &hist_rows, &rel, &colsum, &bin_base, &part_entry, &part_fine,
+                   &sorted_entry, &bucket_start, &run_key, &buckets, &lead_val, &lead_open, &cross_key,
+                   &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T};
+    for (Buf* b : bufs) b->release();
+  }
+};
+
+// One in-flight MSM: its own stream, device workspace, result buffer, captured graphs and events.
+// Two slots let msm_compute_many_device run MSM b+1 while MSM b is still on the device (the
+// latency-bound tails of one overlap the other's kernels) and while the host finishes MSM b
+// (window Horner).
 struct Slot {
+  hipStream_t stream = nullptr;
+  Workspace ws;
   HostBuf h_out;  // k_bucket_reduce_2 writes the window terms, err and total here
   void* h_out_dev = nullptr;
   struct GraphKey {
@@ -151,13 +167,9 @@ constexpr uint32_t PROF_EVERY = 4;
 struct DevCtx {
   int device = -1;
   int n_cu = 256;
-  hipStream_t stream = nullptr;
   std::mutex mu;
-  Buf wire_points, wire_scalars, pts, err, digits, hist_rows, rel, colsum, bin_base;
-  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
-  Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
+  Buf wire_points, wire_scalars;  // staging for host-resident inputs (msm_compute)
   Slot slot[NSLOT];
-  int next_slot = 0;
   uint32_t prof_seq = 0;
   hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
   int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate only (graph-friendly)
@@ -202,10 +214,12 @@ int get_ctx(int device, DevCtx** out) {
       delete c;
       return MSM_ERR_HIP;
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-      delete c;
-      hipSetDevice(prev);
-      return MSM_ERR_HIP;
+    for (Slot& sl : c->slot) {
+      if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        hipSetDevice(prev);
+        return MSM_ERR_HIP;
+      }
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
     for (Slot& sl : c->slot) {
@@ -270,13 +284,15 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
   return MSM_OK;
 }
 
-int ensure_workspace(DevCtx* c, const Plan& pl) {
+int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
+  Slot& sl0 = c->slot[si];
+  Workspace& w = sl0.ws;
   const MsmDims& d = pl.d;
   const size_t nb = (size_t)d.W * d.B;
   int rc;
   const uint64_t gen0 = g_alloc_gen;
 #define ENS(buf, bytes) \
-  if ((rc = c->buf.ensure(bytes)) != MSM_OK) return rc
+  if ((rc = w.buf.ensure(bytes)) != MSM_OK) return rc
   ENS(pts, (size_t)d.n * PRE_WORDS * 4);
   ENS(err, 16);
   ENS(digits, (size_t)d.W * d.n * 4);
@@ -306,19 +322,17 @@ int ensure_workspace(DevCtx* c, const Plan& pl) {
     // err, lead_flag and hist_rows are kept all-zero between MSMs by the kernels themselves
     // (k_bucket_reduce_2 clears the flags, k_part_scatter the histogram rows it consumed), so a
     // replayed graph needs no memset nodes; fresh allocations start that invariant here.
-    if (hipMemsetAsync(c->err.p, 0, c->err.cap, c->stream) != hipSuccess ||
-        hipMemsetAsync(c->lead_flag.p, 0, c->lead_flag.cap, c->stream) != hipSuccess ||
-        hipMemsetAsync(c->skew_list.p, 0, 4, c->stream) != hipSuccess ||
-        hipMemsetAsync(c->hist_rows.p, 0, c->hist_rows.cap, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    hipStream_t st = sl0.stream;
+    if (hipMemsetAsync(w.err.p, 0, w.err.cap, st) != hipSuccess ||
+        hipMemsetAsync(w.lead_flag.p, 0, w.lead_flag.cap, st) != hipSuccess ||
+        hipMemsetAsync(w.skew_list.p, 0, 4, st) != hipSuccess ||
+        hipMemsetAsync(w.hist_rows.p, 0, w.hist_rows.cap, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
       return MSM_ERR_HIP;
   }
   const size_t hbytes = (size_t)d.W * pl.nterms * 32 * 4 + 64;
-  for (Slot& sl : c->slot) {
-    if (hbytes > sl.h_out.cap || !sl.h_out_dev) {
-      if ((rc = sl.h_out.ensure(hbytes)) != MSM_OK) return rc;
-      if (hipHostGetDevicePointer(&sl.h_out_dev, sl.h_out.p, 0) != hipSuccess) return MSM_ERR_HIP;
-    }
+  if (hbytes > sl0.h_out.cap || !sl0.h_out_dev) {
+    if ((rc = sl0.h_out.ensure(hbytes)) != MSM_OK) return rc;
+    if (hipHostGetDevicePointer(&sl0.h_out_dev, sl0.h_out.p, 0) != hipSuccess) return MSM_ERR_HIP;
   }
   return MSM_OK;
 }
@@ -333,71 +347,72 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
                 hipStream_t s, int parts = PART_ALL) {
   const MsmDims& d = pl.d;
   Slot& sl = c->slot[si];
+  Workspace& w = sl.ws;
   const bool prof = c->profiling == 1;
   auto mark = [&](int ph) {
     if (prof) hipEventRecord(c->ev[ph], s);
   };
-  const uint32_t* total = c->bin_base.as<uint32_t>() + d.nbins;
+  const uint32_t* total = w.bin_base.as<uint32_t>() + d.nbins;
   const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
   if (parts & PART_PRE) {
   mark(PH_START);
-  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS)), dim3(PP_THREADS), 0, s, d_points, c->pts.as<uint32_t>(), d.n,
-                     c->err.as<uint32_t>());
+  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS)), dim3(PP_THREADS), 0, s, d_points, w.pts.as<uint32_t>(), d.n,
+                     w.err.as<uint32_t>());
   mark(PH_PREPARE);
   const size_t hist_lds = (size_t)d.W * d.nbc * 4;
   const unsigned rc_grid = grid_for(d.n, RC_SPAN);
   if (d.c <= 16) {
     hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                       c->digits.as<uint16_t>(), c->hist_rows.as<uint32_t>());
+                       w.digits.as<uint16_t>(), w.hist_rows.as<uint32_t>());
   } else {
     hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                       c->digits.as<uint32_t>(), c->hist_rows.as<uint32_t>());
+                       w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
   }
   mark(PH_RECODE);
-  hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, c->hist_rows.as<uint32_t>(), d,
-                     c->rel.as<uint32_t>(), c->colsum.as<uint32_t>());
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, c->colsum.as<uint32_t>(), c->bin_base.as<uint32_t>(),
+  hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
+                     w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
                      d.nbins);
   mark(PH_SCAN);
   if (d.c <= 16) {
     hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                       c->digits.as<uint16_t>(), d, c->hist_rows.as<uint32_t>(), c->rel.as<uint32_t>(),
-                       c->bin_base.as<uint32_t>(), c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+                       w.digits.as<uint16_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
+                       w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
   } else {
     hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                       c->digits.as<uint32_t>(), d, c->hist_rows.as<uint32_t>(), c->rel.as<uint32_t>(),
-                       c->bin_base.as<uint32_t>(), c->part_entry.as<uint32_t>(), c->part_fine.as<uint16_t>());
+                       w.digits.as<uint32_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
+                       w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
   }
   mark(PH_SCATTER);
-  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, c->part_entry.as<uint32_t>(),
-                     c->part_fine.as<uint16_t>(), c->bin_base.as<uint32_t>(), d, pl.K, c->sorted_entry.as<uint32_t>(),
-                     c->bucket_start.as<uint32_t>(), c->run_key.as<uint32_t>());
+  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
+                     w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
+                     w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>());
   mark(PH_FINE);
   }
   if (parts & PART_ACC) {
-  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, c->pts.as<uint32_t>(),
-                     c->sorted_entry.as<uint32_t>(), c->bucket_start.as<uint32_t>(), c->run_key.as<uint32_t>(), total,
-                     pl.K, c->buckets.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->lead_open.as<uint32_t>(),
-                     c->cross_key.as<uint32_t>(), c->skew_list.as<uint32_t>(), c->g_head.as<uint32_t>(),
-                     c->g_hkey.as<uint32_t>(), c->g_tkey.as<uint32_t>());
+  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, w.pts.as<uint32_t>(),
+                     w.sorted_entry.as<uint32_t>(), w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total,
+                     pl.K, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                     w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
+                     w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
   mark(PH_ACCUM);
   }
   if (parts & PART_POST) {
-  hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, c->skew_list.as<uint32_t>(), total, pl.K,
-                     c->g_head.as<uint32_t>(), c->g_hkey.as<uint32_t>(), c->g_tkey.as<uint32_t>(),
-                     c->buckets.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->lead_open.as<uint32_t>(),
-                     c->lead_flag.as<uint32_t>());
-  hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, c->lead_val.as<uint32_t>(),
-                     c->lead_open.as<uint32_t>(), c->lead_flag.as<uint32_t>(), total, pl.K);
+  hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
+                     w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
+                     w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                     w.lead_flag.as<uint32_t>());
+  hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
+                     w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
   mark(PH_FIXUP);
   hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
-                     c->buckets.as<uint32_t>(), c->bucket_start.as<uint32_t>(), d, pl.K,
-                     c->cross_key.as<uint32_t>(), c->lead_val.as<uint32_t>(), c->red_U.as<uint32_t>(),
-                     c->red_T.as<uint32_t>());
+                     w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K,
+                     w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(),
+                     w.red_T.as<uint32_t>());
   mark(PH_RED1);
-  hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, c->red_U.as<uint32_t>(),
-                     c->red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, c->err.as<uint32_t>(),
-                     c->lead_flag.as<uint32_t>(), c->skew_list.as<uint32_t>(), total,
+  hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
+                     w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
+                     w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total,
                      reinterpret_cast<uint32_t*>(sl.h_out_dev));
   mark(PH_RED2);
   mark(PH_READBACK);
@@ -540,10 +555,11 @@ int find_input_nodes(Slot& sl) {
 // re-capture).
 int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points, const uint32_t* d_scalars) {
   const MsmDims& d = pl.d;
+  Workspace& w = sl.ws;
   const uint32_t* wire = d_points;
-  uint32_t* ptsb = c->pts.as<uint32_t>();
+  uint32_t* ptsb = w.pts.as<uint32_t>();
   uint32_t n = d.n;
-  uint32_t* err = c->err.as<uint32_t>();
+  uint32_t* err = w.err.as<uint32_t>();
   void* a_prep[] = {&wire, &ptsb, &n, &err};
   hipKernelNodeParams kp = sl.p_prep;
   kp.kernelParams = a_prep;
@@ -551,8 +567,8 @@ int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points
   if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_prep, &kp) != hipSuccess) return MSM_ERR_HIP;
   const uint32_t* scal = d_scalars;
   MsmDims dd = d;
-  void* digits = c->digits.p;
-  uint32_t* hist = c->hist_rows.as<uint32_t>();
+  void* digits = w.digits.p;
+  uint32_t* hist = w.hist_rows.as<uint32_t>();
   void* a_rc[] = {&scal, &dd, &digits, &hist};
   hipKernelNodeParams kr = sl.p_recode;
   kr.kernelParams = a_rc;
@@ -637,7 +653,7 @@ int submit_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32
   // profiling mode 2 brackets k_accumulate with events on every PROF_EVERY-th MSM only (each
   // bracket costs ~20 us of launch gaps); the mean over those is the reported duration
   sl.bracketed = c->profiling == 2 && (c->prof_seq++ % PROF_EVERY) == 0;
-  int rc = launch_msm(c, pl, d_points, d_scalars, si, s, s == c->stream, sl.bracketed);
+  int rc = launch_msm(c, pl, d_points, d_scalars, si, s, s == sl.stream, sl.bracketed);
   if (rc != MSM_OK) return rc;
   HIPCHECK(hipEventRecord(sl.ev_done, s));
   return MSM_OK;
@@ -705,43 +721,57 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
-  if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
-  hipStream_t s = user_stream ? user_stream : c->stream;
-  const int si = c->next_slot;
-  c->next_slot = (si + 1) % NSLOT;
+  const int si = 0;  // a lone MSM always uses slot 0 (the second workspace only for pipelining)
+  if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
+  hipStream_t s = user_stream ? user_stream : c->slot[si].stream;
   if ((rc = submit_msm(c, pl, d_points, d_scalars, si, s)) != MSM_OK) return rc;
   return finish_msm(c, si, result);
 }
 
-// `count` MSMs of n points each, pipelined: MSM b+1 is enqueued before the host finishes MSM b,
-// so the host tail (window Horner) of one overlaps the device work of the next.
+// `count` MSMs of n points each, pipelined over two slots, each with its own stream and
+// workspace: MSM b+1 is enqueued before the host finishes MSM b, so the host tail (window Horner)
+// of one overlaps the device work of the next, and the two MSMs' kernels may overlap on the
+// device (the latency-bound reduction of one beside the other's sort and accumulation).  With a
+// caller-supplied stream everything runs in order on it.
+// Results go out affine (16 words each) or, with `projective`, as X|Y|T|Z partials (32 words).
 int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* d_scalars, size_t n, size_t count,
-             const msm_opts* o, hipStream_t user_stream, uint32_t* out_xy_be) {
+             const msm_opts* o, hipStream_t user_stream, uint32_t* out_be, bool projective) {
+  auto emit = [&](const Pt& r, size_t b) {
+    if (projective)
+      pt_to_be_xyzt(r, out_be + 32 * b);
+    else
+      pt_to_be_affine(r, out_be + 16 * b);
+  };
   if (n == 0) {
-    for (size_t b = 0; b < count; b++) pt_to_be_affine(pt_identity(), out_xy_be + 16 * b);
+    for (size_t b = 0; b < count; b++) emit(pt_identity(), b);
     return MSM_OK;
   }
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
-  if ((rc = ensure_workspace(c, pl)) != MSM_OK) return rc;
-  hipStream_t s = user_stream ? user_stream : c->stream;
-  int first = c->next_slot;
+  const int nslot = count > 1 ? NSLOT : 1;
+  for (int si = 0; si < nslot; si++)
+    if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
+  auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };
   for (size_t b = 0; b <= count; b++) {
     if (b < count) {
-      if (!d_points[b] || !d_scalars[b]) return MSM_ERR_INVALID_ARG;
-      if ((rc = submit_msm(c, pl, d_points[b], d_scalars[b], (int)((first + b) % NSLOT), s)) != MSM_OK) return rc;
+      const int si = (int)(b % nslot);
+      if (!d_points[b] || !d_scalars[b]) rc = MSM_ERR_INVALID_ARG;
+      else rc = submit_msm(c, pl, d_points[b], d_scalars[b], si, stream_of(si));
+      if (rc != MSM_OK) {
+        for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
+        return rc;
+      }
     }
     if (b >= 1) {
       Pt r;
-      if ((rc = finish_msm(c, (int)((first + b - 1) % NSLOT), &r)) != MSM_OK) {
-        hipStreamSynchronize(s);
+      if ((rc = finish_msm(c, (int)((b - 1) % nslot), &r)) != MSM_OK) {
+        for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
         return rc;
       }
-      pt_to_be_affine(r, out_xy_be + 16 * (b - 1));
+      emit(r, b - 1);
     }
   }
-  c->next_slot = (int)((first + count) % NSLOT);
   return MSM_OK;
 }
 
@@ -775,8 +805,8 @@ int run_host(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, co
   }
   if ((rc = c->wire_points.ensure(n * 128)) != MSM_OK) return rc;
   if ((rc = c->wire_scalars.ensure(n * 32)) != MSM_OK) return rc;
-  HIPCHECK(hipMemcpyAsync(c->wire_points.p, points_be, n * 128, hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(hipMemcpyAsync(c->wire_scalars.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(hipMemcpyAsync(c->wire_points.p, points_be, n * 128, hipMemcpyHostToDevice, c->slot[0].stream));
+  HIPCHECK(hipMemcpyAsync(c->wire_scalars.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->slot[0].stream));
   return run_device(c, c->wire_points.as<uint32_t>(), c->wire_scalars.as<uint32_t>(), n, opts, nullptr, result);
 }
 
@@ -797,13 +827,11 @@ void msm_shutdown(void) {
     int prev = 0;
     hipGetDevice(&prev);
     hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
-    Buf* bufs[] = {&c->wire_points, &c->wire_scalars, &c->pts, &c->err, &c->digits, &c->hist_rows, &c->rel, &c->colsum,
-                   &c->bin_base, &c->part_entry, &c->part_fine, &c->sorted_entry, &c->bucket_start,
-                   &c->run_key, &c->buckets, &c->lead_val, &c->lead_open, &c->cross_key, &c->lead_flag, &c->skew_list, &c->g_head, &c->g_hkey, &c->g_tkey,
-                   &c->red_U, &c->red_T};
-    for (Buf* b : bufs) b->release();
+    for (Slot& sl : c->slot) hipStreamSynchronize(sl.stream);
+    c->wire_points.release();
+    c->wire_scalars.release();
     for (Slot& sl : c->slot) {
+      sl.ws.release();
       drop_graphs(sl);
       sl.h_out.release();
       sl.h_out_dev = nullptr;
@@ -811,7 +839,7 @@ void msm_shutdown(void) {
         if (e) hipEventDestroy(e);
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
-    hipStreamDestroy(c->stream);
+    for (Slot& sl : c->slot) hipStreamDestroy(sl.stream);
     hipSetDevice(prev);
   }
   for (DevCtx*& c : g_ctx) {
@@ -919,7 +947,20 @@ int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* 
   if (rc != MSM_OK) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xy_be);
+  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xy_be, false);
+}
+
+int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be,
+                                    size_t n, size_t count, const msm_opts* opts, void* hip_stream,
+                                    uint32_t* out_xyzt_be) {
+  if (!out_xyzt_be || ((!d_points_be || !d_scalars_be) && count)) return MSM_ERR_INVALID_ARG;
+  if (count == 0) return MSM_OK;
+  DevCtx* c;
+  int rc = with_device(opts, &c);
+  if (rc != MSM_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xyzt_be, true);
 }
 
 int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
@@ -1057,7 +1098,9 @@ int msm_test_point_op(uint32_t op, const uint32_t* p, const uint32_t* q, uint32_
   HIPCHECK(hipMalloc(&dout, n * 128 + 128));
   HIPCHECK(hipMemcpy(dp, p, n * 64, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(dq, q, n * 64, hipMemcpyHostToDevice));
-  if (op == 0)
+  if (op == 3)
+    hipLaunchKernelGGL(k_test_quad, dim3(grid_for(4 * n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);
+  else if (op == 0)
     hipLaunchKernelGGL(k_test_point<0>, dim3(grid_for(n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);
   else if (op == 1)
     hipLaunchKernelGGL(k_test_point<1>, dim3(grid_for(n, 256)), dim3(256), 0, 0, dp, dq, dout, (uint32_t)n);

@@ -527,6 +527,16 @@ __device__ __forceinline__ xyzt load_pt(const uint32_t* __restrict__ src) {
   return p;
 }
 
+__device__ __forceinline__ void store_fe_lds(uint32_t* dst, const fe& a) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) dst[k] = a.v[k];
+}
+__device__ __forceinline__ fe load_fe_lds(const uint32_t* src) {
+  fe a;
+#pragma unroll
+  for (int k = 0; k < NL; k++) a.v[k] = src[k];
+  return a;
+}
 __device__ __forceinline__ void store_pt_lds(uint32_t* dst, const xyzt& p) {
 #pragma unroll
   for (int k = 0; k < NL; k++) {
@@ -857,6 +867,7 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
 // (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
 // entry count.
 constexpr int RED2_THREADS = 1024;
+constexpr uint32_t RED2_QUAD = 256;  // tree levels below this many points use quad-cooperative adds
 extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(const uint32_t* __restrict__ in_U,
                                                                              const uint32_t* __restrict__ in_T,
                                                                              uint32_t nchunks, uint32_t nv,
@@ -881,14 +892,30 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
     acc = live ? pt_add(acc, p) : p;
     live = true;
   }
-  // tree reduce through LDS: upper half hands its point to the lower half each round
-  for (uint32_t half = RED2_THREADS / 2; half >= 1; half >>= 1) {
-    if (threadIdx.x >= half && threadIdx.x < 2 * half) store_pt(sh[threadIdx.x - half], acc);
+  // tree reduce through LDS: upper half hands its point to the lower half each round.  The wide
+  // levels add one point per lane; from RED2_QUAD points down, each add is spread over a quad of
+  // lanes (pt_add_quad: 3 multiply latencies instead of 9) since those levels are latency-bound.
+  for (uint32_t half = RED2_THREADS / 2; half >= RED2_QUAD; half >>= 1) {
+    if (threadIdx.x >= half && threadIdx.x < 2 * half) store_pt_lds(sh[threadIdx.x - half], acc);
     __syncthreads();
-    if (threadIdx.x < half) acc = pt_add(acc, load_pt(sh[threadIdx.x]));
+    if (threadIdx.x < half) acc = pt_add(acc, load_pt_lds(sh[threadIdx.x]));
     __syncthreads();
   }
+  if (threadIdx.x < RED2_QUAD) store_pt_lds(sh[threadIdx.x], acc);
+  __syncthreads();
+  {
+    const uint32_t j = threadIdx.x >> 2, q = threadIdx.x & 3;
+    for (uint32_t half = RED2_QUAD / 2; half >= 1; half >>= 1) {
+      const bool act = j < half;  // uniform across a quad
+      fe res;
+      if (act) res = pt_add_quad(load_fe_lds(&sh[j][q * NL]), load_fe_lds(&sh[j + half][q * NL]));
+      __syncthreads();
+      if (act) store_fe_lds(&sh[j][q * NL], res);
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
+    acc = load_pt_lds(sh[0]);
     uint32_t* o = out_host + (size_t)blockIdx.x * 32;
     fe c4[4] = {fe_to_host_mont(acc.X), fe_to_host_mont(acc.Y), fe_to_host_mont(acc.T), fe_to_host_mont(acc.Z)};
     uint32_t wd[8];
@@ -973,6 +1000,40 @@ __global__ void k_test_point(const uint32_t* __restrict__ p, const uint32_t* __r
     fe_to_words_le(c4[qd], ow);
 #pragma unroll
     for (int k = 0; k < 8; k++) out[(size_t)i * 32 + qd * 8 + k] = ow[k];
+  }
+}
+
+// Quad-cooperative add check: pair i is handled by lanes 4i..4i+3.  Inputs as k_test_point
+// (affine LE words), output X,Y,T,Z std LE words [n][32].
+extern "C" __global__ void k_test_quad(const uint32_t* __restrict__ p, const uint32_t* __restrict__ q,
+                                       uint32_t* __restrict__ out, uint32_t n) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, c = threadIdx.x & 3;
+  const bool live = i < n;
+  const uint32_t ii = live ? i : 0;
+  uint32_t w[4][8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    w[0][k] = p[(size_t)ii * 16 + k];
+    w[1][k] = p[(size_t)ii * 16 + 8 + k];
+    w[2][k] = q[(size_t)ii * 16 + k];
+    w[3][k] = q[(size_t)ii * 16 + 8 + k];
+  }
+  const fe px = fe_to_mont(fe_from_words_le(w[0])), py = fe_to_mont(fe_from_words_le(w[1]));
+  const fe qx = fe_to_mont(fe_from_words_le(w[2])), qy = fe_to_mont(fe_from_words_le(w[3]));
+  const fe pc[4] = {px, py, fe_mul(px, py), fe_one()};
+  const fe qc[4] = {qx, qy, fe_mul(qx, qy), fe_one()};
+  fe a = pc[0], b = qc[0];
+#pragma unroll
+  for (uint32_t k = 1; k < 4; k++) {
+    a = fe_sel(c == k, a, pc[k]);
+    b = fe_sel(c == k, b, qc[k]);
+  }
+  const fe r = pt_add_quad(a, b);
+  uint32_t ow[8];
+  fe_to_words_le(fe_to_std(r), ow);
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[(size_t)i * 32 + c * 8 + k] = ow[k];
   }
 }
 

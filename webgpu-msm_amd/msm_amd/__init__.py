@@ -20,7 +20,7 @@ import numpy as np
 
 __all__ = [
     "MsmError", "MsmOpts", "load", "compute_msm", "compute_msm_wire", "compute_msm_device",
-    "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "combine_partials", "point_add_affine",
+    "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "compute_msm_many_device_partial", "combine_partials", "point_add_affine",
     "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
@@ -92,6 +92,7 @@ def load() -> ctypes.CDLL:
         "msm_compute_device_partial": ([vp, vp, sz, optp, vp, u32p], ctypes.c_int),
         "msm_compute_batch_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
         "msm_compute_many_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_compute_many_device_partial": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
         "msm_combine_partials": ([vp, sz, u32p], ctypes.c_int),
         "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
         "msm_split": ([ctypes.c_uint32, vp, sz, u32p], ctypes.c_int),
@@ -284,6 +285,23 @@ def compute_msm_many_device(points_list, scalars_list, n: int, window_size: Opti
                                      _opts(window_size, run_length, device), stream or None, op),
            "msm_compute_many_device")
     return o[:16 * count].reshape(count, 16)
+
+
+def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_size: Optional[int] = None,
+                                    run_length: Optional[int] = None, device: int = -1,
+                                    stream: int = 0) -> np.ndarray:
+    """compute_msm_many_device, each result as a projective X|Y|T|Z partial: [count][32] BE words."""
+    L = load()
+    count = len(points_list)
+    if len(scalars_list) != count:
+        raise ValueError("points_list and scalars_list differ in length")
+    pp = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in points_list])
+    ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
+    o, op = _out(32 * max(count, 1))
+    _check(L.msm_compute_many_device_partial(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n,
+                                             count, _opts(window_size, run_length, device), stream or None, op),
+           "msm_compute_many_device_partial")
+    return o[:32 * count].reshape(count, 32)
 
 
 def combine_partials(partials: np.ndarray) -> Tuple[int, int]:

@@ -20,7 +20,8 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.ndarray:
-    """all_gather one 32-word partial per rank; returns [world, 32] u32 on every rank."""
+    """all_gather this rank's partial(s) — one [32] or a batch [K, 32] — in ONE collective;
+    returns [world, 32] (or [world, K, 32]) u32 on every rank."""
     import torch
     import torch.distributed as dist
 
@@ -31,6 +32,15 @@ def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t, group=group)
     return np.stack([o.cpu().numpy().view(np.uint32) for o in out])
+
+
+def combine_batch_on_root(parts: np.ndarray, rank: int, root: int = 0):
+    """parts [world, K, 32]: rank `root` joins each of the K MSMs' world partials."""
+    if rank != root:
+        return None
+    from . import combine_partials
+
+    return [combine_partials(parts[:, k, :]) for k in range(parts.shape[1])]
 
 
 def combine_on_root(parts: np.ndarray, rank: int, root: int = 0) -> Optional[Tuple[int, int]]:
@@ -50,3 +60,15 @@ def sharded_msm_device(d_points, d_scalars, n_local: int, rank: int, device=None
     part = compute_msm_device_partial(d_points, d_scalars, n_local, window_size=window_size)
     parts = gather_partials(part, device=device, group=group)
     return combine_on_root(parts, rank)
+
+
+def sharded_msm_many_device(points_list, scalars_list, n_local: int, rank: int, device=None, window_size=None,
+                            group=None):
+    """K sharded MSMs, pipelined: each rank computes its K partials through libmsm's pipelined
+    entry (msm_compute_many_device_partial), then ONE all_gather ships all K x 128 B and rank 0
+    joins them — the exchange is batched across the K independent MSMs."""
+    from . import compute_msm_many_device_partial
+
+    parts = compute_msm_many_device_partial(points_list, scalars_list, n_local, window_size=window_size)
+    gathered = gather_partials(parts, device=device, group=group)
+    return combine_batch_on_root(gathered, rank)
