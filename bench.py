@@ -185,6 +185,7 @@ def main():
             if not ok:
                 print(f"RESULT MISMATCH: got {res}, expected {EXPECTED[n]}", file=sys.stderr)
         ms = elapsed * 1e3 / args.steps
+        acc_iso = float(phase_prof["accumulate"])
         nprof = max(1, int(prof["profiled"]))
         acc = float(prof["accumulate_sum"]) / nprof  # mean k_accumulate duration over the timed MSMs
         dev_total = float(prof["device_total_sum"]) / nprof
@@ -225,12 +226,22 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_accumulate", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
-                         "note": "algorithmic bytes = 160 B x points per launch (SURVEY.md §8d) / avg k_accumulate time; "
-                                 "the kernel is integer-VALU bound, see compute_roofline"},
+                         "kernel_ms_timed": round(acc, 4),
+                         "kernel_ms_isolated": round(acc_iso, 4),
+                         "achieved_isolated": round(algo_bytes / (acc_iso * 1e-3) / 1e9, 2),
+                         "note": "achieved = algorithmic bytes (160 B x points per launch, SURVEY.md §8d) / mean "
+                                 "k_accumulate duration from hipEvents in the timed region (every 4th MSM "
+                                 "bracketed; the pipelined batch overlaps the other slot's kernels, so this is "
+                                 "the shared-GPU duration); *_isolated from one unoverlapped eager pass. traffic "
+                                 "= FETCH_SIZE + WRITE_SIZE per launch (profiles/traffic_latest.json). The "
+                                 "kernel is integer-VALU bound (~87% VALU busy): see compute_roofline"},
             "compute_roofline": {"kernel": "k_accumulate", "achieved_gmodmul_s": round(modmul_rate, 1),
+                                 "achieved_isolated_gmodmul_s": round(entries * 7 / (acc_iso * 1e-3) / 1e9, 1),
                                  "peak_gmodmul_s": 167.7,
                                  "frac": round(modmul_rate / 167.7, 4),
-                                 "note": "peak = measured fe_mul throughput, tools/ubench/fmul_bench.hip"},
+                                 "frac_isolated": round(entries * 7 / (acc_iso * 1e-3) / 1e9 / 167.7, 4),
+                                 "note": "7 field multiplies per accumulated entry (pt_madd); peak = measured fe_mul "
+                                         "throughput, tools/ubench/fmul_bench.hip"},
             "phases_ms": phases,
             "device_ms": round(dev_total, 4),
             "latency_ms": round(float(np.median(lat)) * 1e3, 4),

@@ -13,7 +13,7 @@ pass() {
   local name=$1; shift
   echo "== pass $name: $*" >&2
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- \
-    python bench.py --steps 3 --warmup 1 --no-cpu-baseline "${BENCH_ARGS[@]}" > "$out/$name.log" 2>&1
+    python bench.py --steps 4 --warmup 1 --no-cpu-baseline "${BENCH_ARGS[@]}" > "$out/$name.log" 2>&1
   local rc=$?
   echo "== pass $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then tail -5 "$out/$name.log" >&2; fi

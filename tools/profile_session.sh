@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU tests, bench, and a rocprofv3 kernel-trace summary of a bench run.  Usage: bash tools/profile_session.sh <tag>
+# GPU tests, bench, rocprofv3 kernel-trace summaries of bench runs (pipelined, and single-slot for
+# clean per-kernel durations), and the PMC passes.  Usage: bash tools/profile_session.sh <tag>
 set -u
 tag=${1:-r1}
 mkdir -p gpurun_out
@@ -17,3 +18,8 @@ run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout 600
 run bench 300 python bench.py
 export TMPDIR=/tmp
 run kstats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/kstats_$tag" -o run -- python bench.py --no-cpu-baseline
+MSM_SLOTS=1 run kstats1 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/kstats1_$tag" -o run -- python bench.py --no-cpu-baseline
+if [ "${PMC:-1}" = "1" ]; then
+  run pmc 900 bash tools/profile_pmc.sh "$tag"
+  python tools/pmc_summary.py "gpurun_out/pmc_$tag" 1048576 "gpurun_out/pmc_$tag/traffic.json" > "gpurun_out/pmc_$tag/summary.json" 2>&1 || true
+fi

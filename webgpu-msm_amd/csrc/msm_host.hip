@@ -123,11 +123,11 @@ struct Plan {
 // Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
 struct Workspace {
   Buf pts, err, digits, hist_rows, rel, colsum, bin_base;
-  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
+  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets, big_tiles, cursor;
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
   void release() {
     Buf* bufs[] = {&pts, &err, &digits, &hist_rows, &rel, &colsum, &bin_base, &part_entry, &part_fine,
-                   &sorted_entry, &bucket_start, &run_key, &buckets, &lead_val, &lead_open, &cross_key,
+                   &sorted_entry, &bucket_start, &run_key, &buckets, &big_tiles, &cursor, &lead_val, &lead_open, &cross_key,
                    &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T};
     for (Buf* b : bufs) b->release();
   }
@@ -305,6 +305,8 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(sorted_entry, pl.Mmax * 4);
   ENS(bucket_start, (nb + 2) * 4);
   ENS(run_key, pl.runs_max * 4);
+  ENS(big_tiles, (pl.Mmax / FS_CAP + d.nbins + 1) * 8 + 8);
+  ENS(cursor, nb * 4);
   ENS(buckets, nb * PT_WORDS * 4);
   const size_t nwg = pl.runs_max / ACC_THREADS + 2;
   ENS(lead_val, nwg * PT_WORDS * 4);
@@ -372,7 +374,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
                      w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
-                     d.nbins);
+                     d.nbins, w.big_tiles.as<uint32_t>());
   mark(PH_SCAN);
   if (d.c <= 16) {
     hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
@@ -386,7 +388,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   mark(PH_SCATTER);
   hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
                      w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
-                     w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>());
+                     w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.cursor.as<uint32_t>());
+  hipLaunchKernelGGL(k_big_place, dim3(BP_GRID), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
+                     w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, w.big_tiles.as<uint32_t>(),
+                     w.cursor.as<uint32_t>(), w.sorted_entry.as<uint32_t>());
   mark(PH_FINE);
   }
   if (parts & PART_ACC) {
@@ -749,7 +754,10 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
-  const int nslot = count > 1 ? NSLOT : 1;
+  // MSM_SLOTS=1 keeps the pipelined batch on one stream (kernels never overlap: clean per-kernel
+  // durations for profiling)
+  static const int max_slots = getenv("MSM_SLOTS") && atoi(getenv("MSM_SLOTS")) == 1 ? 1 : NSLOT;
+  const int nslot = count > 1 ? max_slots : 1;
   for (int si = 0; si < nslot; si++)
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };

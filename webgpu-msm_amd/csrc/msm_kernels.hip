@@ -310,10 +310,22 @@ extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t
   }
 }
 
+// k_fine_sort geometry (also decides which bins k_bin_scan lists for k_big_place)
+constexpr uint32_t FS_THREADS = 256;
+constexpr uint32_t FS_R = 24;
+constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS
+constexpr uint32_t FS_MAXF = 2048;
+constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel by k_big_place
+
 // Exclusive scan of colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] = total entries).
+// Also lists the tiles (FS_CAP entries) of bins too big for k_fine_sort's LDS staging:
+// big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
 extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ colsum,
-                                                              uint32_t* __restrict__ bin_base, uint32_t nbins) {
+                                                              uint32_t* __restrict__ bin_base, uint32_t nbins,
+                                                              uint32_t* __restrict__ big_tiles) {
   __shared__ uint32_t part[1024];
+  __shared__ uint32_t ntile;
+  if (threadIdx.x == 0) ntile = 0;
   const uint32_t per = (nbins + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per;
   uint32_t sum = 0;
@@ -330,11 +342,22 @@ extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __
   uint32_t run = part[threadIdx.x] - sum;
   for (uint32_t k = 0; k < per; k++) {
     if (lo + k < nbins) {
+      const uint32_t m = colsum[lo + k];
       bin_base[lo + k] = run;
-      run += colsum[lo + k];
+      run += m;
+      if (m > FS_BIG) {
+        const uint32_t nt = (m + FS_CAP - 1) / FS_CAP;
+        const uint32_t at = atomicAdd(&ntile, nt);
+        for (uint32_t t = 0; t < nt; t++) {
+          big_tiles[1 + 2 * (at + t)] = lo + k;
+          big_tiles[2 + 2 * (at + t)] = t * FS_CAP;
+        }
+      }
     }
   }
   if (threadIdx.x == 1023) bin_base[nbins] = part[1023];
+  __syncthreads();
+  if (threadIdx.x == 0) big_tiles[0] = ntile;
 }
 
 // Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
@@ -399,22 +422,34 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
 }
 
 // Pass 3: one workgroup per coarse bin, counting sort by fine bucket (<= FS_MAXF per bin).  A bin
-// of at most FS_CAP entries is sorted inside LDS and streamed out coalesced; larger bins (skewed
-// scalars) loop over register tiles and scatter directly.  Besides the sorted entry list it
-// writes the bucket boundaries the accumulation walks: bucket_start[key] (global position of
-// bucket `key`'s first entry; bucket_start[W*B] = bucket_start[W*B+1] = total) and
+// of at most FS_CAP entries is sorted inside LDS and streamed out coalesced.  Besides the sorted
+// entry list it writes the bucket boundaries the accumulation walks: bucket_start[key] (global
+// position of bucket `key`'s first entry; bucket_start[W*B] = bucket_start[W*B+1] = total) and
 // run_key[r] = the bucket holding position r*K (the first entry of accumulation run r).
-constexpr uint32_t FS_THREADS = 256;
-constexpr uint32_t FS_R = 24;
-constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS
-constexpr uint32_t FS_MAXF = 2048;
+//
+// A bin of up to FS_BIG entries (e.g. the dense top window) is placed here tile by tile with
+// direct scatters.  A bigger one (skewed scalars) is only counted here -- boundaries, run keys
+// and one placement cursor per bucket -- and its entries are placed by k_big_place, whose
+// workgroups share the bin tile by tile.  Counting collapses runs of equal keys per lane before
+// touching LDS, so a bin that is one giant bucket costs one atomic per lane, not per entry.
+
+__device__ __forceinline__ void count_runs(uint32_t* cnt, uint32_t& last, uint32_t& run, uint32_t key) {
+  if (key == last) {
+    run++;
+  } else {
+    if (run) atomicAdd(&cnt[last], run);
+    last = key;
+    run = 1;
+  }
+}
 
 extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint32_t* __restrict__ part_entry,
                                                                      const uint16_t* __restrict__ part_fine,
                                                                      const uint32_t* __restrict__ bin_base, MsmDims d,
                                                                      uint32_t K, uint32_t* __restrict__ sorted_entry,
                                                                      uint32_t* __restrict__ bucket_start,
-                                                                     uint32_t* __restrict__ run_key) {
+                                                                     uint32_t* __restrict__ run_key,
+                                                                     uint32_t* __restrict__ cursor) {
   __shared__ uint32_t cnt[FS_MAXF];
   __shared__ uint32_t st_entry[FS_CAP];
   const uint32_t bin = blockIdx.x;
@@ -424,19 +459,38 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
   const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
   const uint32_t key0 = w * d.B + (cb << d.fb);
   for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
+  if (bin + 1 == gridDim.x && threadIdx.x == 0) {
+    bucket_start[d.W * d.B] = base + m;
+    bucket_start[d.W * d.B + 1] = base + m;
+  }
   __syncthreads();
   const bool staged = m <= FS_CAP;
   uint32_t fk[FS_R], en[FS_R];
-  for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
+  if (staged) {
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++) {
-      const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
+      const uint32_t e = r * FS_THREADS + threadIdx.x;
       fk[r] = e < m ? part_fine[base + e] : 0xffffu;
-      en[r] = (staged && e < m) ? part_entry[base + e] : 0u;
+      en[r] = e < m ? part_entry[base + e] : 0u;
     }
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++)
       if (fk[r] != 0xffffu) atomicAdd(&cnt[fk[r]], 1u);
+  } else {
+    // register tiles of FS_R keys per lane (independent loads in flight); runs of equal keys
+    // are collapsed before the LDS atomic
+    uint32_t last = 0, run = 0;
+    for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
+#pragma unroll
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
+        fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < FS_R; r++)
+        if (fk[r] != 0xffffu) count_runs(cnt, last, run, fk[r]);
+    }
+    if (run) atomicAdd(&cnt[last], run);
   }
   __syncthreads();
   // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them
@@ -455,40 +509,77 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     if (f < nf) {
       const uint32_t gs = base + cnt[f];
       bucket_start[key0 + f] = gs;
+      if (m > FS_BIG) cursor[key0 + f] = gs;
       if (my_cnt[q]) {
         const uint32_t ge = gs + my_cnt[q];
         for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
       }
     }
   }
-  if (bin + 1 == gridDim.x && threadIdx.x == 0) {
-    bucket_start[d.W * d.B] = base + m;
-    bucket_start[d.W * d.B + 1] = base + m;
-  }
+  if (m > FS_BIG) return;  // k_big_place moves the entries
   __syncthreads();
-  if (staged) {
+  if (!staged) {
+    for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
 #pragma unroll
-    for (uint32_t r = 0; r < FS_R; r++) {
-      if (fk[r] != 0xffffu) {
-        const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
-        st_entry[p] = en[r];
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
+        fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+        en[r] = e < m ? part_entry[base + e] : 0u;
       }
+#pragma unroll
+      for (uint32_t r = 0; r < FS_R; r++)
+        if (fk[r] != 0xffffu) sorted_entry[base + atomicAdd(&cnt[fk[r]], 1u)] = en[r];
     }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
     return;
   }
-  for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
 #pragma unroll
-    for (uint32_t r = 0; r < FS_R; r++) {
-      const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
-      fk[r] = e < m ? part_fine[base + e] : 0xffffu;
-      en[r] = e < m ? part_entry[base + e] : 0u;
+  for (uint32_t r = 0; r < FS_R; r++) {
+    if (fk[r] != 0xffffu) {
+      const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
+      st_entry[p] = en[r];
     }
-#pragma unroll
-    for (uint32_t r = 0; r < FS_R; r++) {
-      if (fk[r] != 0xffffu) sorted_entry[base + atomicAdd(&cnt[fk[r]], 1u)] = en[r];
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
+}
+
+// Placement for bins larger than FS_CAP: workgroups stride over the tiles (FS_CAP entries) of
+// every big bin.  Per tile: LDS histogram of fine keys (runs of equal keys collapsed), one
+// global reservation per (tile, bucket) on the bucket's cursor, then each entry takes the next
+// slot of its bucket's reserved range.  The order inside a bucket is irrelevant to the sum.
+constexpr uint32_t BP_GRID = 512;
+extern "C" __global__ void __launch_bounds__(FS_THREADS) k_big_place(const uint32_t* __restrict__ part_entry,
+                                                                     const uint16_t* __restrict__ part_fine,
+                                                                     const uint32_t* __restrict__ bin_base, MsmDims d,
+                                                                     const uint32_t* __restrict__ big_tiles,
+                                                                     uint32_t* __restrict__ cursor,
+                                                                     uint32_t* __restrict__ sorted_entry) {
+  const uint32_t ntiles = big_tiles[0];
+  if (blockIdx.x >= ntiles) return;
+  __shared__ uint32_t cnt[FS_MAXF];
+  const uint32_t nf = 1u << d.fb;
+  for (uint32_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+    const uint32_t bin = big_tiles[1 + 2 * ti], t0 = big_tiles[2 + 2 * ti];
+    const uint32_t base = bin_base[bin];
+    const uint32_t m = min(bin_base[bin + 1] - base - t0, FS_CAP);
+    const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
+    const uint32_t key0 = w * d.B + (cb << d.fb);
+    for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
+    __syncthreads();
+    uint32_t last = 0, run = 0;
+    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS) count_runs(cnt, last, run, part_fine[base + t0 + e]);
+    if (run) atomicAdd(&cnt[last], run);
+    __syncthreads();
+    for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) {
+      const uint32_t c = cnt[f];
+      if (c) cnt[f] = atomicAdd(&cursor[key0 + f], c);
     }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS) {
+      const uint32_t f = part_fine[base + t0 + e];
+      sorted_entry[atomicAdd(&cnt[f], 1u)] = part_entry[base + t0 + e];
+    }
+    __syncthreads();
   }
 }
 
