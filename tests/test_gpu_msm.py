@@ -289,3 +289,21 @@ def test_many_device_pipelined_distinct_inputs():
     small = M.compute_msm_many_device([cases[1][0]], [cases[1][1]], 100)
     assert (O.be_words_to_int(small[0][:8]), O.be_words_to_int(small[0][8:])) == \
         O.closed_form_msm([4 + 3 * i for i in range(100)], O.xorshift_scalars(100, seed=101))
+
+
+def test_reference_format_test_case(tmp_path):
+    # a case written in the reference's on-disk format (testCases.ts:34-52), z != 1 included
+    from msm_amd import testdata as TD
+
+    n = 3000
+    quads, ks = [], [11 + 7 * i for i in range(n)]
+    base = O.gen_points(n, k0=11, step=7)
+    for i in range(n):
+        x, y = O.be_words_to_int(base[i, :8]), O.be_words_to_int(base[i, 8:16])
+        z = 1 + (i % 5)
+        quads.append((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z))
+    ss = O.xorshift_scalars(n, seed=4242)
+    pp, sp = str(tmp_path / "p.txt"), str(tmp_path / "s.txt")
+    TD.write_test_case(pp, sp, quads, ss)
+    pts, sc = TD.load_test_case(pp, sp)
+    assert M.compute_msm_wire(pts, sc) == O.closed_form_msm(ks, ss)

@@ -17,3 +17,8 @@ export declare const init: () => number;
 export declare const deviceCount: () => number;
 export declare const nUint32PerScalar: 8;
 export declare const nUint32PerPoint: 32;
+export declare const loadTestCase: (
+  pointsPath: string,
+  scalarsPath: string
+) => Promise<{ baseAffinePoints: BigIntPoint[]; scalars: bigint[] }>;
+export declare const expectedPowersResult: Record<16 | 17 | 18 | 19 | 20, { x: bigint; y: bigint }>;

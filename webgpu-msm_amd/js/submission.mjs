@@ -9,6 +9,7 @@
 // argument { windowSize } or the MSM_WINDOW_SIZE environment variable.
 // There is no WebGPU/WGSL/CPU fallback: without the addon or a gfx950 device this rejects.
 import { createRequire } from "module";
+import fs from "fs";
 
 const require = createRequire(import.meta.url);
 const addon = require("./msm_napi.node");
@@ -87,3 +88,32 @@ export const split_dynamic = (windowSize, scalarsU32) => addon.split(windowSize,
 export const point_add_affine = (a16, b16) => addon.pointAddAffine(a16, b16);
 export const init = () => addon.init();
 export const deviceCount = () => addon.deviceCount();
+
+// loadTestCase (src/test-data/testCases.ts:34-52): JSON-lines points whose string fields are
+// BigInts, and one decimal scalar per line.  Paths instead of fetch() URLs (Node, not a browser).
+export const loadTestCase = async (pointsPath, scalarsPath) => {
+  const pointsText = await fs.promises.readFile(pointsPath, "utf8");
+  if (pointsText.startsWith("version https://git-lfs.github.com/spec/v1"))
+    throw new Error(`${pointsPath} is a Git-LFS pointer stub, not the test data`);
+  const baseAffinePoints = pointsText
+    .trim()
+    .split("\n")
+    .filter((l) => l.length)
+    .map((line) => JSON.parse(line, (key, value) => (typeof value === "string" ? BigInt(value) : value)));
+  const scalarsText = await fs.promises.readFile(scalarsPath, "utf8");
+  const scalars = scalarsText
+    .trim()
+    .split("\n")
+    .filter((l) => l.length)
+    .map((line) => BigInt(line));
+  return { baseAffinePoints, scalars };
+};
+
+// Expected results of the reference's 2^16..2^20 cases (testCases.ts:11-32).
+export const expectedPowersResult = {
+  16: { x: 4490298471131273381350715833932091894064554978284853693957586604825823442429n, y: 207233051598812890797414182362695316831408959017076683749810755208551572458n },
+  17: { x: 405755281347735151880827575059343698498813029460786026451708154294960743560n, y: 7112985356832152643523650125935205310677117771129806490701829425450717492869n },
+  18: { x: 4020134989704514076121556080357844499902614818105934254331815581426895427831n, y: 2694327822589008080344499645494473764166611881342421427746308662023437975766n },
+  19: { x: 3856727778963570638772781884183843350150969534777451295534564482755471873113n, y: 1398750101296346671684024297455637342909036274728274942667983346895370713922n },
+  20: { x: 5201851187583570844529445080011852189038251929148722905178398320328749074909n, y: 3586360219804356686204324370397321114669962278596135149389460948678051407803n },
+};
