@@ -923,12 +923,19 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
       if (cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
     }
   }
+  if (!live) {  // whole chunk empty (e.g. the windows above the scalars' top bit)
+    const xyzt id = pt_identity();
+    store_pt(out_U + (size_t)g * PT_WORDS, id);
+    store_pt(out_T + (size_t)g * PT_WORDS, id);
+    return;
+  }
   xyzt carry = pt_identity(), acc = pt_identity();
   bool carry_live = false, acc_live = false;
   // running sums from the top bucket down; the next live bucket's load is issued before the
-  // current bucket's adds
-  int i = 31 - __builtin_clz(live | 1u);
-  xyzt nb = (live >> i) & 1u ? load_pt(buckets + (size_t)(key0 + i) * PT_WORDS) : pt_identity();
+  // current bucket's adds.  (Interleaving the two adds of a step for ILP costs more in VGPRs and
+  // spills than it gains here: measured.)
+  int i = 31 - __builtin_clz(live);
+  xyzt nb = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
 #pragma unroll 1
   for (; i >= 0; i--) {
     if ((live >> i) & 1u) {
@@ -958,7 +965,10 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
 // (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
 // entry count.
 constexpr int RED2_THREADS = 1024;
-constexpr uint32_t RED2_QUAD = 256;  // tree levels below this many points use quad-cooperative adds
+#ifndef MSM_RED2_QUAD
+#define MSM_RED2_QUAD 256
+#endif
+constexpr uint32_t RED2_QUAD = MSM_RED2_QUAD;  // tree levels below this many points use quad-cooperative adds
 extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(const uint32_t* __restrict__ in_U,
                                                                              const uint32_t* __restrict__ in_T,
                                                                              uint32_t nchunks, uint32_t nv,
@@ -973,12 +983,14 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
   const bool vterm = term < nv;
   const uint32_t* src = vterm ? in_U : in_T;
   const uint32_t kbit = term - nv;
-  const uint32_t slice = nchunks / nv;
-  const uint32_t c0 = vterm ? term * slice : 0, c1 = vterm ? c0 + slice : nchunks;
+  // Every term sums exactly nchunks/2 points (a V slice, or the chunks with bit k set), and the
+  // j-th of them is enumerated directly, so every lane loads the same number of points (a
+  // stride-and-skip loop over all chunks would give half the lanes all the work for k < 10).
+  const uint32_t half_n = nchunks / 2;
   xyzt acc = pt_identity();
   bool live = false;
-  for (uint32_t c = c0 + threadIdx.x; c < c1; c += RED2_THREADS) {
-    if (!vterm && !((c >> kbit) & 1u)) continue;
+  for (uint32_t j = threadIdx.x; j < (nv == 1 && vterm ? nchunks : half_n); j += RED2_THREADS) {
+    const uint32_t c = vterm ? term * half_n + j : (((j >> kbit) << (kbit + 1)) | (1u << kbit) | (j & ((1u << kbit) - 1u)));
     xyzt p = load_pt(src + ((size_t)w * nchunks + c) * PT_WORDS);
     acc = live ? pt_add(acc, p) : p;
     live = true;
