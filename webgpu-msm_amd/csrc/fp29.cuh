@@ -61,12 +61,14 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
 #ifndef MSM_SEED_ASM
 #define MSM_SEED_ASM 1
 #endif
-// a * b + 1 as one v_mad_u64_u32 with an inline-constant addend (carry-out discarded into an
-// unused SGPR pair).
-__device__ __forceinline__ uint64_t mad64_seed1(uint32_t a, uint32_t b) {
-  uint64_t r, unused;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 1" : "=v"(r), "=s"(unused) : "v"(a), "v"(b));
-  return r;
+// The constant 1 as an opaque VGPR value (hoisted, one register per kernel).  Used as the
+// pre-seeded carry of fe_mul's columns: with a literal 1, LLVM's reassociation moves the constant
+// out of each column's multiply-add chain into a separate 64-bit add (and an inline-asm
+// v_mad_u64_u32 with a literal addend costs hazard NOPs around every asm block instead).
+__device__ __forceinline__ uint64_t opaque_one() {
+  uint32_t r;
+  asm("v_mov_b32 %0, 1" : "=v"(r));
+  return (uint64_t)r;
 }
 
 __device__ __forceinline__ void fe_set(fe& r, const uint32_t* c) {
@@ -96,12 +98,11 @@ __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   uint64_t c[2 * NL];
 #if MSM_SEED_ASM
-  // The first product of each seeded column carries the +1 as its inline-constant addend.  In
-  // plain C, LLVM reassociates the constant out of the accumulation chain into a separate 64-bit
-  // add per column; the asm result is opaque, so the chain stays put.
+  // The first product of each seeded column carries the +1 (opaque_one) as its addend.
+  const uint64_t one = opaque_one();
 #pragma unroll
-  for (int k = 0; k < NL; k++) c[k] = k == 0 ? (uint64_t)a.v[0] * b.v[0] : mad64_seed1(a.v[0], b.v[k]);
-  c[NL] = mad64_seed1(a.v[1], b.v[NL - 1]);
+  for (int k = 0; k < NL; k++) c[k] = k == 0 ? (uint64_t)a.v[0] * b.v[0] : mad64(a.v[0], b.v[k], one);
+  c[NL] = mad64(a.v[1], b.v[NL - 1], one);
 #pragma unroll
   for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
 #pragma unroll
