@@ -6,7 +6,7 @@ column overflow would be a silent, data-dependent wrong answer that random tests
 never, so this test walks every formula in the kernels with per-limb worst-case bounds (interval
 arithmetic on the limb maxima) and asserts:
 
-  * every fe_mul column stays < 2^64 (products + reduction terms + seed + incoming carry);
+  * every fe_mul column stays < 2^64 (products + reduction terms + incoming carry);
   * every fe_mul operand pair keeps a*b < p * 2^261, so the lazy result is < 2p (no final
     subtraction needed);
   * fe_sub / fe_neg never produce a negative limb (K8P dominates the subtrahend limb-wise).
@@ -47,8 +47,7 @@ def fe_mul(a: B, b: B) -> B:
     for i in range(NL):
         for j in range(NL):
             cols[i + j] += a.l[i] * b.l[j]
-    for k in range(1, NL + 1):
-        cols[k] += 1  # pre-seeded carries
+    cols[NL] += 1  # the one seeded product (the last reduction step's carry +1)
     carry = 0
     for k in range(2 * NL):
         red = 0
@@ -56,6 +55,8 @@ def fe_mul(a: B, b: B) -> B:
             j = k - i
             if 1 <= j < NL and i < NL:
                 red += (1 << LB) * P29[j]
+        # columns 1..8 hold their value minus the (un-added) +1 of the incoming carry, which is
+        # <= the true column, so bounding the true column (carry + 1) bounds the register too
         col = cols[k] + red + carry
         assert col < 1 << 64, f"column {k} may reach {col / 2**64:.3f} * 2^64"
         carry = (col >> LB) + 1

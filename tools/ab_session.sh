@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B session: GPU tests on the default build, then bench for each library variant given.
-# Usage: bash tools/ab_session.sh libA.so libB.so ...   (paths relative to webgpu-msm_amd/msm_amd/_lib)
+# A/B session: ISA issue rates + library-variant sweep.  Stops at the first crash/timeout.
+#   bash tools/ab_session.sh <libs> [extra sweep args]
 set -u
 mkdir -p gpurun_out
 run() {
@@ -9,11 +9,10 @@ run() {
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
   local rc=$?
   echo "== $name rc=$rc" >&2
-  tail -n 15 "gpurun_out/$name.txt" >&2
+  tail -n 20 "gpurun_out/$name.txt" >&2
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)" >&2; exit $rc; fi
   return 0
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout 600
-for v in "$@"; do
-  MSM_AMD_LIB=$PWD/webgpu-msm_amd/msm_amd/_lib/$v run bench_$v 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
-done
+libs=$1; shift
+if [ -x tools/ubench/isa_rates ] && [ "${ISA_RATES:-0}" = 1 ]; then run isa_rates 120 tools/ubench/isa_rates; fi
+run sweep 600 python tools/sweep.py --libs "$libs" --windows 16 --runs 64 --steps 30 "$@"

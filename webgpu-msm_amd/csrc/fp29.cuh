@@ -58,17 +58,11 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * b + c;
 }
 
-#ifndef MSM_SEED_ASM
-#define MSM_SEED_ASM 1
-#endif
-// The constant 1 as an opaque VGPR value (hoisted, one register per kernel).  Used as the
-// pre-seeded carry of fe_mul's columns: with a literal 1, LLVM's reassociation moves the constant
-// out of each column's multiply-add chain into a separate 64-bit add (and an inline-asm
-// v_mad_u64_u32 with a literal addend costs hazard NOPs around every asm block instead).
-__device__ __forceinline__ uint64_t opaque_one() {
-  uint32_t r;
-  asm("v_mov_b32 %0, 1" : "=v"(r));
-  return (uint64_t)r;
+// Pins a seeded product: an empty asm on the result keeps LLVM from reassociating the seed out
+// of the multiply-add (it would otherwise add it separately, one 64-bit add per column).
+__device__ __forceinline__ uint64_t seeded(uint64_t x) {
+  asm("" : "+v"(x));
+  return x;
 }
 
 __device__ __forceinline__ void fe_set(fe& r, const uint32_t* c) {
@@ -89,43 +83,31 @@ __device__ __forceinline__ fe fe_zero() {
 __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 
 // Montgomery product a*b*2^-261 mod p (result normalised, value < 2p when a,b < 2^257).
-// Reduction digit m' = 2^29 - (column mod 2^29) in [1, 2^29] instead of the textbook
-// (-column) mod 2^29: it still zeroes the column, and the carry it produces is always exactly
-// (column >> 29) + 1, so the nine "+1"s are pre-seeded into columns 1..9 and each step needs no
-// 64-bit "column += m" (saves a zero-extension move and a half-rate 64-bit add per step).
-// Column bound with the larger digit: <= 0.95 * 2^64 for unnormalised-sub x S operands
-// (tests/golden bounds check).
+// Reduction digits, with p = 1 (mod 2^29) (so m * p_0 = m):
+//  * step 0: m_0 = 2^29 - (c_0 mod 2^29) in [1, 2^29]; it zeroes column 0 and carries exactly
+//    (c_0 >> 29) + 1.
+//  * steps 1..8 see their column "biased": the +1 of the previous carry is not added, so the
+//    register holds s_i = column_i - 1 (>= 0: every carry is >= 1).  Then m_i = ~s_i mod 2^29
+//    = 2^29 - 1 - (s_i mod 2^29) (one v_bfi_b32) again zeroes the column, whose carry is
+//    (s_i >> 29) + 1, and the +1 is again left as the next column's bias.
+//  * the last step's +1 lands in column 9 (the result's limb 0): one seeded product.
+// m_i <= 2^29 as before, so column bounds are unchanged (tests/test_limb_bounds.py).
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   uint64_t c[2 * NL];
-#if MSM_SEED_ASM
-  // The first product of each seeded column carries the +1 (opaque_one) as its addend.
-  const uint64_t one = opaque_one();
 #pragma unroll
-  for (int k = 0; k < NL; k++) c[k] = k == 0 ? (uint64_t)a.v[0] * b.v[0] : mad64(a.v[0], b.v[k], one);
-  c[NL] = mad64(a.v[1], b.v[NL - 1], one);
-#pragma unroll
-  for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
+  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
+  c[NL] = seeded(mad64(a.v[1], b.v[NL - 1], 1));
 #pragma unroll
   for (int i = 0; i < NL; i++)
 #pragma unroll
     for (int j = 0; j < NL; j++) {
-      if (i == 0 || (i == 1 && j == NL - 1)) continue;  // already issued as seeded products
+      if (i == 1 && j == NL - 1) continue;  // issued above as the seeded product
       c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
     }
-#else
-  c[0] = 0;
-#pragma unroll
-  for (int k = 1; k <= NL; k++) c[k] = 1;
-#pragma unroll
-  for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++)
-#pragma unroll
-    for (int j = 0; j < NL; j++) c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
-#endif
 #pragma unroll
   for (int i = 0; i < NL; i++) {
-    const uint32_t m = (1u << LBITS) - ((uint32_t)c[i] & LMASK);
+    const uint32_t lo = (uint32_t)c[i];
+    const uint32_t m = i == 0 ? (1u << LBITS) - (lo & LMASK) : (~lo & LMASK);
     c[i + 1] += c[i] >> LBITS;
 #pragma unroll
     for (int j = 1; j < NL; j++) c[i + j] = mad64(m, P29[j], c[i + j]);
