@@ -6,11 +6,19 @@
 namespace msm {
 
 // Geometry of one MSM launch (host fills it, kernels read it by value).
+// Windows (balanced widths): W - 1 "main" windows cover scalar bits [0, 254) -- the first nhi of
+// them q + 1 bits wide, the rest q bits -- and one 3-bit overflow window covers bits [254, 256)
+// plus the carry.  A scalar < 2^253 (any canonical Fr/Fq value) never carries out of the top main
+// window, so the overflow window only holds digits of non-canonical 256-bit scalars.  Balancing
+// keeps the top main window as wide as the others (a ragged top window of a few bits would turn
+// into a handful of giant buckets).
 struct MsmDims {
   uint32_t n;      // points
-  uint32_t c;      // window bits
-  uint32_t B;      // buckets per window = 2^(c-1) (signed digits)
-  uint32_t W;      // windows = ceil(257 / c)
+  uint32_t c;      // widest window (bits); digit codes and bucket tables are sized for it
+  uint32_t B;      // buckets per window = 2^(c-1) (signed digits; narrower windows use fewer)
+  uint32_t W;      // windows, overflow window included
+  uint32_t q;      // main-window base width
+  uint32_t nhi;    // main windows of width q + 1
   uint32_t fb;     // fine bits sorted inside one coarse bin = min(c-1, 9)
   uint32_t nbc;    // coarse bins per window = B >> fb
   uint32_t nbins;  // W * nbc
@@ -18,6 +26,17 @@ struct MsmDims {
   uint32_t nch;    // chunks per window = ceil(n / ch)
 };
 
+
+constexpr uint32_t MAIN_BITS = 254;  // bits covered by the main windows (scalars < 2^253, + carry)
+constexpr uint32_t OVF_BITS = 3;     // overflow window: bits 254, 255 and the carry (digit <= 4)
+
+// Width and bit offset of window w.
+__host__ __device__ inline uint32_t win_bits(const MsmDims& d, uint32_t w) {
+  return w + 1 == d.W ? OVF_BITS : (w < d.nhi ? d.q + 1 : d.q);
+}
+__host__ __device__ inline uint32_t win_off(const MsmDims& d, uint32_t w) {
+  return w * d.q + (w < d.nhi ? w : d.nhi);
+}
 
 constexpr uint32_t PT_WORDS = 36;  // extended point, 4 x 9 limbs (144 B)
 constexpr uint32_t PRE_WORDS = 32;  // precomputed affine point record (108 B used, 128 B stride)

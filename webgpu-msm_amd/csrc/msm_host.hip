@@ -161,7 +161,7 @@ struct Slot {
   Plan pl{};
   bool bracketed = false;
 };
-constexpr int NSLOT = 2;
+constexpr int NSLOT = 4;  // at most this many MSMs in flight (one HIP stream each)
 constexpr uint32_t PROF_EVERY = 4;
 
 struct DevCtx {
@@ -253,8 +253,13 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
   MsmDims d;
   d.n = (uint32_t)n;
   d.c = c;
-  d.B = 1u << (c - 1);
-  d.W = (257 + c - 1) / c;
+  // balanced main windows of at most c bits over MAIN_BITS, plus the overflow window
+  const uint32_t wm = (MAIN_BITS + c - 1) / c;
+  d.q = MAIN_BITS / wm;
+  d.nhi = MAIN_BITS - d.q * wm;
+  d.W = wm + 1;
+  d.c = d.nhi ? d.q + 1 : d.q;
+  d.B = 1u << (d.c - 1);
   // Coarse bins: aim at ~4K entries per bin (half the LDS staging capacity of k_fine_sort) with at
   // most FS_MAXF buckets per bin.  Partition chunks hold >= 64 entries per bin slice.
   uint32_t nbc = 1;
@@ -397,7 +402,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   if (parts & PART_ACC) {
   hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, w.pts.as<uint32_t>(),
                      w.sorted_entry.as<uint32_t>(), w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total,
-                     pl.K, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                     pl.K, d.W * d.B, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
                      w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
                      w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
   mark(PH_ACCUM);
@@ -444,7 +449,7 @@ Pt horner_tail(const Plan& pl, const uint32_t* terms) {
       Fq X;
       memcpy(X.l, o, 32);
       if (fq_is_zero(X) && !memcmp(o + 8, o + 24, 32)) continue;  // identity: X = 0, Y = Z
-      pos.push_back(d.c * (uint32_t)w + ((uint32_t)t < pl.nv ? 0u : pl.lgL + ((uint32_t)t - pl.nv)));
+      pos.push_back(win_off(d, (uint32_t)w) + ((uint32_t)t < pl.nv ? 0u : pl.lgL + ((uint32_t)t - pl.nv)));
       idx.push_back(i);
     }
   Pt acc = pt_identity();
@@ -733,10 +738,20 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   return finish_msm(c, si, result);
 }
 
-// `count` MSMs of n points each, pipelined over two slots, each with its own stream and
-// workspace: MSM b+1 is enqueued before the host finishes MSM b, so the host tail (window Horner)
-// of one overlaps the device work of the next, and the two MSMs' kernels may overlap on the
-// device (the latency-bound reduction of one beside the other's sort and accumulation).  With a
+// MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
+// and sort kernels leave most of the chip idle), so more of them run side by side; MSM_SLOTS
+// overrides (1 = everything in order on one stream: clean per-kernel profiles).
+int pipeline_slots(size_t n) {
+  static const int env = getenv("MSM_SLOTS") ? atoi(getenv("MSM_SLOTS")) : 0;
+  if (env >= 1) return std::min(env, NSLOT);
+  (void)n;
+  return 3;  // measured best at 2^16..2^20 (4 streams contend for the hardware queues)
+}
+
+// `count` MSMs of n points each, pipelined over pipeline_slots(n) slots, each with its own stream
+// and workspace: later MSMs are enqueued before the host finishes MSM b, so the host tail (window
+// Horner) of one overlaps the device work of the next, and the MSMs' kernels may overlap on the
+// device (the latency-bound reduction of one beside another's sort and accumulation).  With a
 // caller-supplied stream everything runs in order on it.
 // Results go out affine (16 words each) or, with `projective`, as X|Y|T|Z partials (32 words).
 int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* d_scalars, size_t n, size_t count,
@@ -754,14 +769,13 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
-  // MSM_SLOTS=1 keeps the pipelined batch on one stream (kernels never overlap: clean per-kernel
-  // durations for profiling)
-  static const int max_slots = getenv("MSM_SLOTS") && atoi(getenv("MSM_SLOTS")) == 1 ? 1 : NSLOT;
-  const int nslot = count > 1 ? max_slots : 1;
+  const int nslot = count > 1 ? (int)std::min<size_t>(count, (size_t)pipeline_slots(n)) : 1;
   for (int si = 0; si < nslot; si++)
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };
-  for (size_t b = 0; b <= count; b++) {
+  // MSM b goes to slot b % nslot once MSM b - nslot (its previous occupant) is finished; MSM
+  // b - nslot + 1 is finished right after b is enqueued, so nslot MSMs are in flight.
+  for (size_t b = 0; b < count + nslot - 1; b++) {
     if (b < count) {
       const int si = (int)(b % nslot);
       if (!d_points[b] || !d_scalars[b]) rc = MSM_ERR_INVALID_ARG;
@@ -771,13 +785,14 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
         return rc;
       }
     }
-    if (b >= 1) {
+    if (b + 1 >= (size_t)nslot) {
+      const size_t f = b + 1 - nslot;
       Pt r;
-      if ((rc = finish_msm(c, (int)((b - 1) % nslot), &r)) != MSM_OK) {
+      if ((rc = finish_msm(c, (int)(f % nslot), &r)) != MSM_OK) {
         for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
         return rc;
       }
-      emit(r, b - 1);
+      emit(r, f);
     }
   }
   return MSM_OK;
@@ -876,21 +891,14 @@ const char* msm_strerror(int code) {
 }
 
 uint32_t msm_best_window(size_t n) {
-  // Signed digits: cost ~ W*n (accumulation) + ~2*W*2^(c-1) (bucket running sums) weighted by
-  // the reduction's lower parallelism.  Pick the minimum over c in [8, 16].
-  if (n == 0) return 8;
-  double best = 1e300;
-  uint32_t bc = 8;
-  for (uint32_t c = 8; c <= 16; c++) {
-    double W = (257.0 + c - 1) / c;
-    W = (double)(uint32_t)W;
-    double cost = W * (double)n + 3.0 * W * (double)(1u << (c - 1));
-    if (cost < best) {
-      best = cost;
-      bc = c;
-    }
-  }
-  return bc;
+  // Measured on MI355X (tools/tune_session.sh, balanced windows): c = 16 is fastest from 2^16 to
+  // 2^20 -- the bucket reduction is latency-bound, so its cost hardly grows with 2^c, while
+  // every extra window adds n entries and narrow windows make dense, chained buckets.  Below
+  // that, keep ~8+ entries per bucket; the bucket tables (W * 2^(c-1) points) shrink with c.
+  if (n >= (1u << 15)) return 16;
+  uint32_t c = 8;
+  while (c < 16 && (size_t)(1u << (c + 3)) <= n) c++;
+  return c;
 }
 
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,

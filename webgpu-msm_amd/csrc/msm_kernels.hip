@@ -161,22 +161,24 @@ __device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32
 // ---------------------------------------------------------------------------------------------
 // scalar recoding
 // ---------------------------------------------------------------------------------------------
-// Signed recoding of one scalar (little-endian words, consumed in place).  Calls f(window, digit)
-// for every window, digit in [-(2^(c-1)-1), 2^(c-1)]; sum_w digit_w 2^(c w) == scalar exactly
-// (W = ceil(257/c) windows).  The scalar is shifted down c bits per window with v_alignbit so no
-// register array is ever indexed dynamically (that would spill it to scratch).
+// Signed recoding of one scalar (little-endian words, consumed in place).  Calls f(window,
+// digit) for every window, digit in [-(2^(b-1)-1), 2^(b-1)] for a window of b bits (win_bits);
+// sum_w digit_w 2^win_off(w) == scalar exactly.  The scalar is shifted down b bits per window
+// with v_alignbit so no register array is ever indexed dynamically (that would spill it to
+// scratch).
 template <typename F>
 __device__ __forceinline__ void recode(uint32_t s[8], const MsmDims& d, F&& f) {
-  const uint32_t mask = (1u << d.c) - 1u;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < d.W; w++) {
-    const uint32_t v = (s[0] & mask) + carry;
+    const uint32_t b = win_bits(d, w);
+    const uint32_t half = 1u << (b - 1);
+    const uint32_t v = (s[0] & ((1u << b) - 1u)) + carry;
 #pragma unroll
-    for (int q = 0; q < 7; q++) s[q] = __builtin_amdgcn_alignbit(s[q + 1], s[q], d.c);
-    s[7] >>= d.c;
+    for (int q = 0; q < 7; q++) s[q] = __builtin_amdgcn_alignbit(s[q + 1], s[q], b);
+    s[7] >>= b;
     int32_t digit;
-    if (v > d.B) {
-      digit = (int32_t)v - (int32_t)(2 * d.B);
+    if (v > half) {
+      digit = (int32_t)v - (int32_t)(2 * half);
       carry = 1;
     } else {
       digit = (int32_t)v;
@@ -649,6 +651,29 @@ __device__ __forceinline__ xyzt load_pt_lds(const uint32_t* src) {
   return p;
 }
 
+// First bucket key k > cur whose end bucket_start[k + 1] lies past pos, given that bucket cur is
+// empty (bucket_start[cur + 1] == pos).  bucket_start is non-decreasing and ends with the total
+// (> pos), so an exponential search then a binary search find it in O(log gap) loads: a window
+// narrower than the bucket table, or a stretch of empty windows (small or structured scalars),
+// would otherwise cost one dependent load per empty bucket.
+__device__ __forceinline__ uint32_t next_nonempty(const uint32_t* __restrict__ bucket_start, uint32_t cur, uint32_t pos,
+                                               uint32_t nkeys) {
+  uint32_t lo = cur, step = 1;  // bucket lo is empty
+  uint32_t hi = cur + 1;        // bucket nkeys - 1 ends at the total (> pos): the search stops there
+  while (bucket_start[hi + 1] == pos) {
+    lo = hi;
+    step <<= 1;
+    hi = min(cur + step, nkeys - 1);
+  }
+  // bucket lo empty, bucket hi ends past pos: the answer is in (lo, hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (bucket_start[mid + 1] == pos) lo = mid;
+    else hi = mid;
+  }
+  return hi;
+}
+
 // Bucket accumulation over the sorted list.  Lane = run of K consecutive entries (perfect load
 // balance whatever the bucket sizes).  Inside a run, whole buckets are written straight to the
 // bucket table; bucket boundaries come from bucket_start (one load per bucket, issued a bucket
@@ -673,6 +698,7 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
                                                                        const uint32_t* __restrict__ bucket_start,
                                                                        const uint32_t* __restrict__ run_key,
                                                                        const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                                                       uint32_t nkeys,
                                                                        uint32_t* __restrict__ buckets,
                                                                        uint32_t* __restrict__ lead_val,
                                                                        uint32_t* __restrict__ lead_open,
@@ -706,12 +732,15 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
         } else {
           store_pt(buckets + (size_t)cur * PT_WORDS, acc);
         }
-        // advance to the next non-empty bucket
-        do {
-          cur++;
-          bend = bnext;
+        // advance to the next non-empty bucket (a run of empty ones is skipped by galloping)
+        cur++;
+        bend = bnext;
+        bnext = bucket_start[cur + 2];
+        if (bend == pos) {
+          cur = next_nonempty(bucket_start, cur, pos, nkeys);
+          bend = bucket_start[cur + 1];
           bnext = bucket_start[cur + 2];
-        } while (bend == pos);
+        }
         acc = pt_identity();
         seg_first = false;
       }
