@@ -763,14 +763,21 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   const uint32_t last = min(ACC_THREADS, nruns - min(nruns, blockIdx.x * ACC_THREADS)) - 1;
   if (lt == last) cross_key[blockIdx.x] = cont ? cur : KEY_INVALID;
   __syncthreads();
-  // Chains of heads: a run whose head is "pass" continues into the next run.  Runs of two or more
-  // pass heads in a row (dense buckets: skewed scalars, or the sparse top window) are deferred
-  // to k_chain_join's logarithmic scan; otherwise every chain has at most one pass head and is
-  // joined right here with at most two adds.
+  // Chains of heads: a run whose head is "pass" continues into the next run.  Runs of three or
+  // more pass heads in a row (buckets of ~200+ entries: skewed scalars), and a lead chain that
+  // leaves the workgroup, are deferred to k_chain_join's logarithmic scan; otherwise every chain
+  // has at most two pass heads and is joined right here with at most three adds.  (The top
+  // window of canonical scalars holds ~110 entries per bucket, so two-pass chains are common.)
   const uint32_t hk = sh_hkey[lt];
+  auto is_pass = [&](uint32_t r) {
+    const uint32_t k = sh_hkey[r];
+    return k != KEY_INVALID && (k & KEY_PASS) != 0;
+  };
   const bool my_pass = hk != KEY_INVALID && (hk & KEY_PASS);
-  const bool nxt_pass = lt < last && (sh_hkey[lt + 1] & KEY_PASS) && sh_hkey[lt + 1] != KEY_INVALID;
-  if (__syncthreads_or((my_pass && nxt_pass) || (lt == 0 && my_pass))) {
+  const bool nxt_pass = lt < last && is_pass(lt + 1);
+  const bool nxt2_pass = lt + 1 < last && is_pass(lt + 2);
+  if (__syncthreads_or((my_pass && nxt_pass && nxt2_pass) ||
+                       (lt == 0 && my_pass && (last == 0 || (nxt_pass && last == 1))))) {
     // skewed workgroup: stage heads and tail pieces for k_chain_join
     if (s < M) {
       g_hkey[t] = hk;
@@ -781,19 +788,28 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
     if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = blockIdx.x;
     return;
   }
-  // lane 0's head (never pass here) is the end of the previous workgroup's crossing bucket
+  // Lane 0's head is the end of the previous workgroup's crossing bucket: the workgroup's lead.
+  // If it is pass-through (a bucket spanning run 0 whole), the bucket ends in run 1 or 2 (not
+  // past the workgroup here), and lane 0 joins those heads into the lead.
+  const bool lead_join = lt == 0 && my_pass;
   if (lt == 0) {
     lead_open[blockIdx.x] = 0u;
-    if (s < M && hk != KEY_INVALID) store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
+    if (s < M && hk != KEY_INVALID && !lead_join)
+      store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
   }
-  if (has_tail) {
-    // the bucket continues in run lt+1 (and lt+2 if lt+1 is pass-through), unless it leaves the
-    // workgroup: then k_bucket_reduce_1 adds the next workgroup's lead (cross_key).  (Two
-    // straight-line adds: the same in a loop costs ~50 more VGPRs and occupancy.)
-    const uint32_t nwalk = lt < last ? 1u + ((nxt_pass && lt + 1 < last) ? 1u : 0u) : 0u;
+  if (has_tail || lead_join) {
+    // a tail's bucket continues in run lt+1 (and lt+2, lt+3 while those are pass-through), unless
+    // it leaves the workgroup: then k_bucket_reduce_1 adds the next workgroup's lead
+    // (cross_key).  (Straight-line adds: the same in a loop costs ~50 more VGPRs and occupancy.)
+    const uint32_t nwalk =
+        lead_join ? 1u + (nxt_pass ? 1u : 0u)
+                  : (lt < last ? 1u + ((nxt_pass && lt + 1 < last) ? 1u + ((nxt2_pass && lt + 2 < last) ? 1u : 0u) : 0u)
+                               : 0u);
+    if (lead_join) acc = load_pt_lds(sh_head[0]);
     if (nwalk) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
     if (nwalk > 1) acc = pt_add(acc, load_pt_lds(sh_head[lt + 2]));
-    store_pt(buckets + (size_t)cur * PT_WORDS, acc);
+    if (nwalk > 2) acc = pt_add(acc, load_pt_lds(sh_head[lt + 3]));
+    store_pt(lead_join ? lead_val + (size_t)blockIdx.x * PT_WORDS : buckets + (size_t)cur * PT_WORDS, acc);
   }
 }
 
