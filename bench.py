@@ -19,6 +19,9 @@ computes its K partial points (pipelined the same way), the K x 128 B partials a
 over RCCL (torch.distributed "nccl") in one collective and rank 0 adds each step's N partials:
 strong scaling of the MSM (BASELINE configs[3]).  Rank 0 prints ONE JSON line.
 MSM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU.
+
+--batch B (e.g. --batch 64 --n 262144, BASELINE configs[4]) instead times steps of B independent
+MSMs over one fixed base vector, dealt round-robin to the ranks (replicas, no collective).
 """
 import argparse
 import json
@@ -55,7 +58,67 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-logn", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--batch", type=int, default=0,
+                    help="prover-batch mode (BASELINE configs[4], e.g. --batch 64 --n 262144): a step is B "
+                         "independent n-point MSMs over one fixed base vector, dealt round-robin to the ranks")
     return ap.parse_args()
+
+
+def batch_bench(args, world, rank, dev, gather_dev):
+    """BASELINE configs[4]: B independent MSMs per step (fixed bases P_i = (i+1)G, per-MSM scalar
+    streams seeded XORSHIFT_SEED + b).  Replicas only: rank r runs MSMs b = r, r + world, ...
+    through libmsm's pipelined entry; no data-path collective (the results stay on their rank).
+    Correctness: every rank recomputes its first MSM through the unpipelined single-MSM entry
+    and compares; MSM 0 at 2^16 / 2^20 is also checked against the survey-recorded value."""
+    import torch
+    import torch.distributed as dist
+    import msm_amd as M
+
+    n, B = args.n, args.batch
+    mine = list(range(rank, B, world))
+    d_pts = torch.from_numpy(M.gen_points(n).view(np.int32)).to(dev)
+    d_sc = [torch.from_numpy(M.gen_scalars(n, seed=M.XORSHIFT_SEED + b).view(np.int32)).to(dev) for b in mine]
+    torch.cuda.synchronize()
+
+    def step():
+        return M.compute_msm_many_device([d_pts] * len(mine), d_sc, n) if mine else None
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ok = True
+    if mine:
+        single = M.compute_msm_device(d_pts, d_sc[0], n)
+        ok = (M.wire_to_int(out[0][:8]), M.wire_to_int(out[0][8:])) == single
+        if rank == 0 and n in EXPECTED:
+            ok = ok and single == EXPECTED[n]
+    if world > 1:
+        tt = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=gather_dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, ok = float(tt[0].item()), float(tt[1].item()) == 0.0
+    if rank == 0:
+        ms = elapsed * 1e3 / args.steps
+        lg = int(np.log2(n))
+        print(json.dumps({
+            "metric": f"ms per batch of {B} independent 2^{lg}-point MSMs (prover-batch shape, BASELINE configs[4])",
+            "value": round(ms, 4), "unit": "ms/batch", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 4), "ms_per_msm": round(ms / B, 4), "higher_is_better": False,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32 (29-bit-limb Montgomery Fq, 253-bit)",
+            "data": "synthetic: P_i=(i+1)G shared by the batch, xorshift64 scalars seeded per MSM",
+            "config": {"workload": f"{B} x 2^{lg}-point Edwards-BLS12 MSMs, replicas over {world} GPU(s)",
+                       "n_points": n, "batch": B, "parallelism": f"replicas{world}"},
+            "correct": ok}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(args):
@@ -115,6 +178,9 @@ def main():
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     gather_dev = dev if backend != "gloo" else None
+    if args.batch:
+        batch_bench(args, world, rank, dev, gather_dev)
+        return
 
     from msm_amd.dist import shard_range, sharded_msm_device, sharded_msm_many_device
 

@@ -246,8 +246,19 @@ uint32_t ilog2(uint32_t v) {
   return r;
 }
 
-int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl) {
-  uint32_t c = (o && o->window_bits) ? o->window_bits : msm_best_window(n);
+// Window width for MSMs kept in flight by the pipelined entries (whole-job throughput rather
+// than one MSM's latency): there the bucket reduction's work, not its latency, is what counts,
+// so sub-2^20 sizes prefer narrower windows.  Measured on MI355X (tools/window_sweep.sh): c = 14
+// at 2^16, 15 at 2^17..2^19 (-16% at 2^17 vs c = 16), 16 from 2^20.
+uint32_t pipelined_window(size_t n) {
+  if (n >= (1u << 20)) return 16;
+  if (n >= (1u << 17)) return 15;
+  if (n >= (1u << 15)) return 14;
+  return msm_best_window(n);
+}
+
+int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false) {
+  uint32_t c = (o && o->window_bits) ? o->window_bits : pipelined ? pipelined_window(n) : msm_best_window(n);
   if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
   if (n >= (1ull << 30)) return MSM_ERR_INVALID_ARG;
   MsmDims d;
@@ -767,7 +778,7 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
     return MSM_OK;
   }
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl);
+  int rc = make_plan(n, o, c->n_cu, &pl, count > 1);
   if (rc != MSM_OK) return rc;
   const int nslot = count > 1 ? (int)std::min<size_t>(count, (size_t)pipeline_slots(n)) : 1;
   for (int si = 0; si < nslot; si++)
