@@ -246,8 +246,14 @@ struct DigitCode<uint32_t> {
 // each window is one contiguous array) and builds, in LDS, their histogram over every window's
 // nbc coarse bins, flushed with global atomics into hist_rows[w][chunk][bin] (zeroed first).
 // Digits are read back only once, by k_part_scatter.
-constexpr uint32_t PT_THREADS = 1024;
-constexpr uint32_t PS_R = 16;  // digits per lane (ch = PT_THREADS * PS_R)
+#ifndef MSM_PT_THREADS
+#define MSM_PT_THREADS 1024
+#endif
+#ifndef MSM_PS_R
+#define MSM_PS_R 16
+#endif
+constexpr uint32_t PT_THREADS = MSM_PT_THREADS;
+constexpr uint32_t PS_R = MSM_PS_R;  // digits per lane (ch = PT_THREADS * PS_R)
 constexpr uint32_t RC_THREADS = 1024;
 constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup (4 per lane)
 template <typename T>
@@ -1009,7 +1015,10 @@ extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32
 // straight into coherent pinned host memory (no readback copy), so the host Horner
 // (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
 // entry count.
-constexpr int RED2_THREADS = 1024;
+#ifndef MSM_RED2_THREADS
+#define MSM_RED2_THREADS 512
+#endif
+constexpr int RED2_THREADS = MSM_RED2_THREADS;
 #ifndef MSM_RED2_QUAD
 #define MSM_RED2_QUAD 256
 #endif
