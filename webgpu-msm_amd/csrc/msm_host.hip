@@ -681,8 +681,10 @@ int submit_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32
 }
 
 // Wait for the MSM in slot `si` (spinning briefly: the result is usually due within a couple of
-// milliseconds, and a blocking wait adds a wake-up latency), then run its host tail.
-int finish_msm(DevCtx* c, int si, Pt* result) {
+// milliseconds, and a blocking wait adds a wake-up latency) and take its window terms.  With
+// `terms` the terms are copied out, so the slot can take its next MSM before the host tail runs
+// (finish_terms); otherwise the host tail runs here, on the pinned buffer.
+int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr) {
   Slot& sl = c->slot[si];
   const Plan& pl = sl.pl;
   const auto spin_until = clk::now() + std::chrono::milliseconds(50);
@@ -697,7 +699,10 @@ int finish_msm(DevCtx* c, int si, Pt* result) {
   if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
   if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
   auto t0 = clk::now();
-  *result = horner_tail(pl, h);
+  if (terms)
+    terms->assign(h, h + outb / 4);
+  else
+    *result = horner_tail(pl, h);
   auto t1 = clk::now();
   if (c->profiling == 1 || (c->profiling == 2 && sl.bracketed)) {
     float ms[PH_COUNT] = {};
@@ -784,27 +789,26 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
   for (int si = 0; si < nslot; si++)
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };
-  // MSM b goes to slot b % nslot once MSM b - nslot (its previous occupant) is finished; MSM
-  // b - nslot + 1 is finished right after b is enqueued, so nslot MSMs are in flight.
-  for (size_t b = 0; b < count + nslot - 1; b++) {
+  // MSM b goes to slot b % nslot.  Its previous occupant, MSM b - nslot, is waited for and its
+  // window terms copied out just before; the host tail (window Horner) of MSM b - nslot runs
+  // after b is enqueued, so the device holds nslot MSMs while the host works (otherwise MSMs
+  // that finish together leave the device idle for a Horner each).
+  std::vector<uint32_t> terms;
+  auto fail = [&](int code) {
+    for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
+    return code;
+  };
+  for (size_t b = 0; b < count + nslot; b++) {
+    const bool have = b >= (size_t)nslot;
+    const size_t f = have ? b - nslot : 0;
+    if (have && (rc = finish_msm(c, (int)(f % nslot), nullptr, &terms)) != MSM_OK) return fail(rc);
     if (b < count) {
       const int si = (int)(b % nslot);
       if (!d_points[b] || !d_scalars[b]) rc = MSM_ERR_INVALID_ARG;
       else rc = submit_msm(c, pl, d_points[b], d_scalars[b], si, stream_of(si));
-      if (rc != MSM_OK) {
-        for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
-        return rc;
-      }
+      if (rc != MSM_OK) return fail(rc);
     }
-    if (b + 1 >= (size_t)nslot) {
-      const size_t f = b + 1 - nslot;
-      Pt r;
-      if ((rc = finish_msm(c, (int)(f % nslot), &r)) != MSM_OK) {
-        for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
-        return rc;
-      }
-      emit(r, f);
-    }
+    if (have) emit(horner_tail(pl, terms.data()), f);
   }
   return MSM_OK;
 }
