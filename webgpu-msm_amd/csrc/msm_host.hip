@@ -318,7 +318,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(bin_base, ((size_t)d.nbins + 1) * 4);
   ENS(part_entry, pl.Mmax * 4);
   ENS(part_fine, pl.Mmax * 2);
-  ENS(sorted_entry, pl.Mmax * 4);
+  ENS(sorted_entry, pl.Mmax * 4 + 16);  // + a 16-B tail for k_accumulate's vector entry loads
   ENS(bucket_start, (nb + 2) * 4);
   ENS(run_key, pl.runs_max * 4);
   ENS(big_tiles, (pl.Mmax / FS_CAP + d.nbins + 1) * 8 + 8);

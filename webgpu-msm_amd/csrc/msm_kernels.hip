@@ -698,6 +698,9 @@ __device__ __forceinline__ uint32_t next_nonempty(const uint32_t* __restrict__ b
 // the tail owner stores its part in the bucket table and cross_key[g] names the bucket;
 // k_bucket_reduce_1 adds lead_val[g+1] to it, after k_lead_scan has chained leads that
 // themselves run through whole workgroups.
+#ifndef MSM_ACC_VEC
+#define MSM_ACC_VEC 1
+#endif
 constexpr uint32_t ACC_THREADS = 256;
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
                                                                        const uint32_t* __restrict__ sorted_entry,
@@ -730,7 +733,17 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
     uint32_t bend = bucket_start[cur + 1];   // end of bucket `cur`
     uint32_t bnext = bucket_start[cur + 2];  // end of the bucket after it (prefetched)
     bool seg_first = true;
+#if MSM_ACC_VEC
+    // sorted entries four at a time (one 16-B load per lane every fourth step: the lanes walk
+    // runs K entries apart, so scalar loads cost one cache-line request per lane per step)
+    const bool vec = (K & 3u) == 0;  // run starts (t K) are then 16-B aligned
+    uint4 eb = make_uint4(0u, 0u, 0u, 0u);
+#endif
     for (uint32_t pos = s; pos < e; pos++) {
+#if MSM_ACC_VEC
+      const uint32_t jq = (pos - s) & 3u;  // uniform across the lanes still in the loop
+      if (vec && jq == 0) eb = *reinterpret_cast<const uint4*>(sorted_entry + pos);
+#endif
       if (pos == bend) {
         if (seg_first && started_before) {
           store_pt_lds(sh_head[lt], acc);
@@ -750,7 +763,11 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
         acc = pt_identity();
         seg_first = false;
       }
+#if MSM_ACC_VEC
+      const uint32_t ent = !vec ? sorted_entry[pos] : jq == 0 ? eb.x : jq == 1 ? eb.y : jq == 2 ? eb.z : eb.w;
+#else
       const uint32_t ent = sorted_entry[pos];
+#endif
       pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
       acc = pt_madd(acc, q);
     }
