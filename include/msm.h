@@ -90,9 +90,10 @@ int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scal
                              const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
 
 /* `count` independent MSMs of n points each, inputs given by per-MSM device pointers; results
- * [count][16].  Pipelined: MSM b+1 runs on the device while the host finishes MSM b (window
- * Horner), so throughput exceeds 1 / latency.  msm_compute_batch_device is this with contiguous
- * inputs. */
+ * [count][16].  Pipelined: three MSMs stay on the device while the host finishes earlier ones
+ * (window Horner), so throughput exceeds 1 / latency.  With window_bits = 0 the window is tuned
+ * for throughput, which below 2^20 points is narrower than msm_best_window's (same results).
+ * msm_compute_batch_device is this with contiguous inputs. */
 int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
                             size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
 /* Same, each result as a projective X|Y|T|Z partial ([count][32] words) for a later

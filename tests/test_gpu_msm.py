@@ -291,6 +291,31 @@ def test_many_device_pipelined_distinct_inputs():
         O.closed_form_msm([4 + 3 * i for i in range(100)], O.xorshift_scalars(100, seed=101))
 
 
+@pytest.mark.parametrize("logn", [16, 17])
+def test_many_device_throughput_window(logn):
+    # below 2^20 the pipelined entry picks a narrower window than a lone MSM (c = 14 at 2^16,
+    # 15 at 2^17: msm_host.hip pipelined_window); results must not depend on it
+    torch = pytest.importorskip("torch")
+    n = 1 << logn
+    d_pts = torch.from_numpy(O.gen_points(n, k0=1, step=1).view(np.int32)).cuda()
+    scs, exps = [], []
+    for j in range(4):
+        ss = O.xorshift_scalars(n, seed=700 + j)
+        scs.append(torch.from_numpy(O.ints_to_be_words(ss).view(np.int32)).cuda())
+        exps.append(O.closed_form_msm(range(1, n + 1), ss))
+    torch.cuda.synchronize()
+    M.set_profiling(2)  # records the plan of the bracketed (first) MSM
+    try:
+        out = M.compute_msm_many_device([d_pts] * 4, scs, n)
+        prof = M.last_profile()
+    finally:
+        M.set_profiling(False)
+    assert prof["window_bits"] == {16: 14, 17: 15}[logn]
+    for r, exp in zip(out, exps):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == exp
+    assert M.compute_msm_device(d_pts, scs[0], n) == exps[0]  # lone MSM: c = 16
+
+
 def test_reference_format_test_case(tmp_path):
     # a case written in the reference's on-disk format (testCases.ts:34-52), z != 1 included
     from msm_amd import testdata as TD

@@ -134,9 +134,9 @@ struct Workspace {
 };
 
 // One in-flight MSM: its own stream, device workspace, result buffer, captured graphs and events.
-// Two slots let msm_compute_many_device run MSM b+1 while MSM b is still on the device (the
-// latency-bound tails of one overlap the other's kernels) and while the host finishes MSM b
-// (window Horner).
+// Several slots let msm_compute_many_device keep MSMs b+1.. on the device while MSM b is still
+// there (the latency-bound tails of one overlap the others' kernels) and while the host
+// finishes MSM b (window Horner).
 struct Slot {
   hipStream_t stream = nullptr;
   Workspace ws;
@@ -906,7 +906,7 @@ const char* msm_strerror(int code) {
 }
 
 uint32_t msm_best_window(size_t n) {
-  // Measured on MI355X (tools/tune_session.sh, balanced windows): c = 16 is fastest from 2^16 to
+  // Measured on MI355X (tools/window_sweep.sh, balanced windows): c = 16 is fastest from 2^16 to
   // 2^20 -- the bucket reduction is latency-bound, so its cost hardly grows with 2^c, while
   // every extra window adds n entries and narrow windows make dense, chained buckets.  Below
   // that, keep ~8+ entries per bucket; the bucket tables (W * 2^(c-1) points) shrink with c.

@@ -6,7 +6,9 @@
 //               scalars: bigint[] | Uint32Array[]) => Promise<{ x: bigint, y: bigint }>
 //
 // The browser-only knobs (?windowSize=, submission.ts:29-33) become an optional third
-// argument { windowSize } or the MSM_WINDOW_SIZE environment variable.
+// argument { windowSize } or the MSM_WINDOW_SIZE environment variable.  { cpuWorkRatio }
+// (?cpuWorkRatio, submission.ts:96-154) is accepted and the whole MSM runs on the GPU: the host
+// would take ~1000x longer for its share, and the result is the same.
 // There is no WebGPU/WGSL/CPU fallback: without the addon or a gfx950 device this rejects.
 import { createRequire } from "module";
 import fs from "fs";
