@@ -288,7 +288,8 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   while (kauto > 16 && (size_t)d.W * n / kauto < 262144) kauto >>= 1;
   pl->K = (o && o->run_length) ? o->run_length : kauto;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
-  pl->L = RED_L;
+  static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
+  pl->L = l_env == 4 ? 4u : 8u;  // L = 4 measured no faster at any size (tools/l_sweep.sh)
   pl->lgL = ilog2(pl->L);
   pl->nchunks = d.B / pl->L;
   // every k_bucket_reduce_2 workgroup sums at most nchunks/2 points (the R_k terms' size)
@@ -426,10 +427,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
                      w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
   mark(PH_FIXUP);
-  hipLaunchKernelGGL(k_bucket_reduce_1, dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s,
-                     w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K,
-                     w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(),
-                     w.red_T.as<uint32_t>());
+  hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : k_bucket_reduce_1<8>,
+                     dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s, w.buckets.as<uint32_t>(),
+                     w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(),
+                     w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());
   mark(PH_RED1);
   hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
                      w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),

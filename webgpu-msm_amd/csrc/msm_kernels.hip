@@ -965,27 +965,28 @@ extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* _
 //   chunk c (L buckets): U_c = sum_i (i+1) B_{cL+i}, T_c = sum_i B_{cL+i}   (running sums)
 //   G_w = sum_c U_c + L * sum_c c T_c = R_{w,V} + sum_k 2^(lgL+k) R_{w,k},  R_{w,k} = sum_{c: bit k} T_c
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t RED_L = 8;  // buckets per k_bucket_reduce_1 lane (c >= 4 gives B >= 8)
-extern "C" __global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
-                                                                    const uint32_t* __restrict__ bucket_start, MsmDims d,
-                                                                    uint32_t K,
-                                                                    const uint32_t* __restrict__ cross_key,
-                                                                    const uint32_t* __restrict__ lead_val,
-                                                                    uint32_t* __restrict__ out_U,
-                                                                    uint32_t* __restrict__ out_T) {
-  const uint32_t nchunks = d.B / RED_L;
+// L = buckets per k_bucket_reduce_1 lane (8; c >= 4 gives B >= 8).  L = 4 halves each lane's
+// running-sum chain but doubles the R_k trees of k_bucket_reduce_2: measured no faster at any
+// size, so it is only an experiment switch (MSM_RED_L=4).
+template <uint32_t RL>
+__global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
+                                                         const uint32_t* __restrict__ bucket_start, MsmDims d,
+                                                         uint32_t K, const uint32_t* __restrict__ cross_key,
+                                                         const uint32_t* __restrict__ lead_val,
+                                                         uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
+  const uint32_t nchunks = d.B / RL;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= d.W * nchunks) return;
   const uint32_t w = g / nchunks, c = g % nchunks;
-  const uint32_t key0 = w * d.B + c * RED_L;
+  const uint32_t key0 = w * d.B + c * RL;
   // bucket metadata up front (independent loads): which buckets are non-empty, and which left
   // their accumulation workgroup and need the continuation from lead_val
-  uint32_t bs[RED_L + 1];
+  uint32_t bs[RL + 1];
 #pragma unroll
-  for (uint32_t i = 0; i <= RED_L; i++) bs[i] = bucket_start[key0 + i];
+  for (uint32_t i = 0; i <= RL; i++) bs[i] = bucket_start[key0 + i];
   uint32_t live = 0, cross = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < RED_L; i++) {
+  for (uint32_t i = 0; i < RL; i++) {
     if (bs[i + 1] != bs[i]) {
       live |= 1u << i;
       if (cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
