@@ -428,7 +428,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
                      w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
   mark(PH_FIXUP);
   hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : k_bucket_reduce_1<8>,
-                     dim3(grid_for((size_t)d.W * pl.nchunks, 256)), dim3(256), 0, s, w.buckets.as<uint32_t>(),
+                     dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s, w.buckets.as<uint32_t>(),
                      w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(),
                      w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());
   mark(PH_RED1);

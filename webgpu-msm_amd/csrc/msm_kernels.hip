@@ -56,7 +56,10 @@ __device__ __forceinline__ fe load_fe(const uint32_t* src) {
 // instruction); each lane then works on its own point out of LDS.  The 16-B slots of a record are
 // XOR-swizzled by the record index so the per-lane 128-B-strided LDS reads and writes are free of
 // bank conflicts.
-constexpr uint32_t PP_THREADS = 256;
+#ifndef MSM_PP_THREADS
+#define MSM_PP_THREADS 256
+#endif
+constexpr uint32_t PP_THREADS = MSM_PP_THREADS;
 __device__ __forceinline__ uint32_t pp_slot(uint32_t rec, uint32_t q) { return rec * 8 + (q ^ (rec & 7)); }
 
 extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(const uint32_t* __restrict__ wire,
@@ -254,7 +257,10 @@ struct DigitCode<uint32_t> {
 #endif
 constexpr uint32_t PT_THREADS = MSM_PT_THREADS;
 constexpr uint32_t PS_R = MSM_PS_R;  // digits per lane (ch = PT_THREADS * PS_R)
-constexpr uint32_t RC_THREADS = 1024;
+#ifndef MSM_RC_THREADS
+#define MSM_RC_THREADS 1024
+#endif
+constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
 constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup (4 per lane)
 template <typename T>
 __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(const uint32_t* __restrict__ scalars, MsmDims d,
@@ -971,8 +977,12 @@ extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* _
 // L = buckets per k_bucket_reduce_1 lane (8; c >= 4 gives B >= 8).  L = 4 halves each lane's
 // running-sum chain but doubles the R_k trees of k_bucket_reduce_2: measured no faster at any
 // size, so it is only an experiment switch (MSM_RED_L=4).
+#ifndef MSM_RED1_THREADS
+#define MSM_RED1_THREADS 256
+#endif
+constexpr uint32_t RED1_THREADS = MSM_RED1_THREADS;
 template <uint32_t RL>
-__global__ void __launch_bounds__(256) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
+__global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
                                                          const uint32_t* __restrict__ bucket_start, MsmDims d,
                                                          uint32_t K, const uint32_t* __restrict__ cross_key,
                                                          const uint32_t* __restrict__ lead_val,
