@@ -12,11 +12,20 @@ namespace msm {
 // window, so the overflow window only holds digits of non-canonical 256-bit scalars.  Balancing
 // keeps the top main window as wide as the others (a ragged top window of a few bits would turn
 // into a handful of giant buckets).
+// A launch may carry a BATCH of nm independent MSMs of n points each (small MSMs fill the machine
+// together): MSM m owns windows [m Wm, (m+1) Wm) and point records [m n, (m+1) n); every kernel
+// after the recode sees W = nm Wm windows and does not care which MSM a window belongs to.
+constexpr uint32_t MSM_MAX_BATCH = 4;
+struct BatchPtrs {  // per-MSM input buffers of a batch (kernel argument, by value)
+  const uint32_t* p[MSM_MAX_BATCH];
+};
 struct MsmDims {
-  uint32_t n;      // points
+  uint32_t n;      // points per MSM
   uint32_t c;      // widest window (bits); digit codes and bucket tables are sized for it
   uint32_t B;      // buckets per window = 2^(c-1) (signed digits; narrower windows use fewer)
-  uint32_t W;      // windows, overflow window included
+  uint32_t W;      // windows of the whole batch = nm * Wm
+  uint32_t Wm;     // windows per MSM, overflow window included
+  uint32_t nm;     // MSMs in the batch
   uint32_t q;      // main-window base width
   uint32_t nhi;    // main windows of width q + 1
   uint32_t fb;     // fine bits sorted inside one coarse bin = min(c-1, 9)
@@ -30,9 +39,9 @@ struct MsmDims {
 constexpr uint32_t MAIN_BITS = 254;  // bits covered by the main windows (scalars < 2^253, + carry)
 constexpr uint32_t OVF_BITS = 3;     // overflow window: bits 254, 255 and the carry (digit <= 4)
 
-// Width and bit offset of window w.
+// Width and bit offset of window w (w < Wm: a window of one MSM).
 __host__ __device__ inline uint32_t win_bits(const MsmDims& d, uint32_t w) {
-  return w + 1 == d.W ? OVF_BITS : (w < d.nhi ? d.q + 1 : d.q);
+  return w + 1 == d.Wm ? OVF_BITS : (w < d.nhi ? d.q + 1 : d.q);
 }
 __host__ __device__ inline uint32_t win_off(const MsmDims& d, uint32_t w) {
   return w * d.q + (w < d.nhi ? w : d.nhi);

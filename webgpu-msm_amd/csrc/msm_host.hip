@@ -144,11 +144,11 @@ struct Slot {
   void* h_out_dev = nullptr;
   struct GraphKey {
     size_t n;
-    uint32_t c, K;
+    uint32_t c, K, nm;
     int prof;
     uint64_t gen;
     bool operator==(const GraphKey& o) const {
-      return n == o.n && c == o.c && K == o.K && prof == o.prof && gen == o.gen;
+      return n == o.n && c == o.c && K == o.K && nm == o.nm && prof == o.prof && gen == o.gen;
     }
   } gkey{};
   hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
@@ -156,7 +156,7 @@ struct Slot {
   // the two kernel nodes (in graph[0]) that take the MSM's input buffers: repointed per launch
   hipGraphNode_t n_prep = nullptr, n_recode = nullptr;
   hipKernelNodeParams p_prep{}, p_recode{};
-  const void *g_pts = nullptr, *g_sc = nullptr;  // inputs the instantiated graph currently reads
+  BatchPtrs g_pts{}, g_sc{};  // inputs the instantiated graph currently reads
   hipEvent_t ev_start = nullptr, ev_acc0 = nullptr, ev_acc1 = nullptr, ev_end = nullptr, ev_done = nullptr;
   Plan pl{};
   bool bracketed = false;
@@ -257,7 +257,7 @@ uint32_t pipelined_window(size_t n) {
   return msm_best_window(n);
 }
 
-int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false) {
+int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1) {
   uint32_t c = (o && o->window_bits) ? o->window_bits : pipelined ? pipelined_window(n) : msm_best_window(n);
   if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
   if (n >= (1ull << 30)) return MSM_ERR_INVALID_ARG;
@@ -268,7 +268,9 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   const uint32_t wm = (MAIN_BITS + c - 1) / c;
   d.q = MAIN_BITS / wm;
   d.nhi = MAIN_BITS - d.q * wm;
-  d.W = wm + 1;
+  d.Wm = wm + 1;
+  d.nm = nm;
+  d.W = d.Wm * nm;
   d.c = d.nhi ? d.q + 1 : d.q;
   d.B = 1u << (d.c - 1);
   // Coarse bins: aim at ~4K entries per bin (half the LDS staging capacity of k_fine_sort) with at
@@ -310,7 +312,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   const uint64_t gen0 = g_alloc_gen;
 #define ENS(buf, bytes) \
   if ((rc = w.buf.ensure(bytes)) != MSM_OK) return rc
-  ENS(pts, (size_t)d.n * PRE_WORDS * 4);
+  ENS(pts, (size_t)d.nm * d.n * PRE_WORDS * 4);
   ENS(err, 16);
   ENS(digits, (size_t)d.W * d.n * 4);
   ENS(hist_rows, (size_t)d.nch * d.nbins * 4);
@@ -362,7 +364,7 @@ inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((th
 // PART_PRE: memsets, point preparation and the sort; PART_ACC: bucket accumulation;
 // PART_POST: fixup and bucket reduction.
 constexpr int PART_PRE = 1, PART_ACC = 2, PART_POST = 4, PART_ALL = 7;
-int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si,
+int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
                 hipStream_t s, int parts = PART_ALL) {
   const MsmDims& d = pl.d;
   Slot& sl = c->slot[si];
@@ -375,16 +377,16 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
   const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
   if (parts & PART_PRE) {
   mark(PH_START);
-  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS)), dim3(PP_THREADS), 0, s, d_points, w.pts.as<uint32_t>(), d.n,
+  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.nm), dim3(PP_THREADS), 0, s, d_points, w.pts.as<uint32_t>(), d.n,
                      w.err.as<uint32_t>());
   mark(PH_PREPARE);
-  const size_t hist_lds = (size_t)d.W * d.nbc * 4;
+  const size_t hist_lds = (size_t)d.Wm * d.nbc * 4;
   const unsigned rc_grid = grid_for(d.n, RC_SPAN);
   if (d.c <= 16) {
-    hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+    hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
                        w.digits.as<uint16_t>(), w.hist_rows.as<uint32_t>());
   } else {
-    hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+    hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
                        w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
   }
   mark(PH_RECODE);
@@ -447,14 +449,15 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint3
 // positions).  Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then
 // into_affine.  The device already emitted the terms in this file's Montgomery form
 // (fe_to_host_mont).  Runs of doublings skip T (pt_dbl_proj) except the one feeding an add.
-Pt horner_tail(const Plan& pl, const uint32_t* terms) {
+Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
   const MsmDims& d = pl.d;
+  terms += (size_t)m * d.Wm * pl.nterms * 32;  // MSM m's windows
   // terms in descending bit position: windows from the top, inside a window R_k from the top
   // down to the V slices (position 0)
   std::vector<uint32_t> pos, idx;
-  pos.reserve((size_t)d.W * pl.nterms);
-  idx.reserve((size_t)d.W * pl.nterms);
-  for (int w = (int)d.W - 1; w >= 0; w--)
+  pos.reserve((size_t)d.Wm * pl.nterms);
+  idx.reserve((size_t)d.Wm * pl.nterms);
+  for (int w = (int)d.Wm - 1; w >= 0; w--)
     for (int t = (int)pl.nterms - 1; t >= 0; t--) {
       const uint32_t i = (uint32_t)w * pl.nterms + (uint32_t)t;
       const uint32_t* o = terms + (size_t)i * 32;
@@ -523,10 +526,10 @@ void drop_graphs(Slot& sl) {
     sl.graph[i] = nullptr;
   }
   sl.n_prep = sl.n_recode = nullptr;
-  sl.g_pts = sl.g_sc = nullptr;
+  sl.g_pts = sl.g_sc = BatchPtrs{};
 }
 
-int capture(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si, hipStream_t s,
+int capture(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, hipStream_t s,
             int parts, hipGraph_t* gout, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return MSM_ERR_HIP;
@@ -575,10 +578,10 @@ int find_input_nodes(Slot& sl) {
 
 // Point the instantiated slot graph at new input buffers (kernel-node argument update, no
 // re-capture).
-int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points, const uint32_t* d_scalars) {
+int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const BatchPtrs& d_points, const BatchPtrs& d_scalars) {
   const MsmDims& d = pl.d;
   Workspace& w = sl.ws;
-  const uint32_t* wire = d_points;
+  BatchPtrs wire = d_points;
   uint32_t* ptsb = w.pts.as<uint32_t>();
   uint32_t n = d.n;
   uint32_t* err = w.err.as<uint32_t>();
@@ -587,7 +590,7 @@ int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points
   kp.kernelParams = a_prep;
   kp.extra = nullptr;
   if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_prep, &kp) != hipSuccess) return MSM_ERR_HIP;
-  const uint32_t* scal = d_scalars;
+  BatchPtrs scal = d_scalars;
   MsmDims dd = d;
   void* digits = w.digits.p;
   uint32_t* hist = w.hist_rows.as<uint32_t>();
@@ -606,13 +609,15 @@ int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const uint32_t* d_points
 // kernel nodes.  Profiling mode 1 launches eagerly with an event between every phase; mode 2
 // brackets an eager k_accumulate launch with events, between two graphs (pre / post).  Captures
 // only on the library's own stream (a caller's stream may be capturing or in use).
-int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si, hipStream_t s,
+bool same_ptrs(const BatchPtrs& a, const BatchPtrs& b) { return memcmp(&a, &b, sizeof(BatchPtrs)) == 0; }
+
+int launch_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, hipStream_t s,
                bool own_stream, bool bracket) {
   Slot& sl = c->slot[si];
   const int prof = bracket ? 2 : 0;
   const bool graphs = own_stream && c->graphs_ok && graphs_enabled() && c->profiling != 1;
   if (graphs) {
-    Slot::GraphKey key{(size_t)pl.d.n, pl.d.c, pl.K, prof, g_alloc_gen};
+    Slot::GraphKey key{(size_t)pl.d.n, pl.d.c, pl.K, pl.d.nm, prof, g_alloc_gen};
     if (!(sl.gexec[0] && key == sl.gkey)) {
       drop_graphs(sl);
       int rc;
@@ -632,7 +637,7 @@ int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32
         sl.g_sc = d_scalars;
       }
     }
-    if (c->graphs_ok && (sl.g_pts != d_points || sl.g_sc != d_scalars) &&
+    if (c->graphs_ok && (!same_ptrs(sl.g_pts, d_points) || !same_ptrs(sl.g_sc, d_scalars)) &&
         repoint_inputs(c, pl, sl, d_points, d_scalars) != MSM_OK) {
       drop_graphs(sl);
       (void)hipGetLastError();
@@ -668,7 +673,7 @@ int launch_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32
 }
 
 // Start one MSM (device-resident inputs) in slot `si`; returns once it is enqueued.
-int submit_msm(DevCtx* c, const Plan& pl, const uint32_t* d_points, const uint32_t* d_scalars, int si,
+int submit_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
                hipStream_t s) {
   Slot& sl = c->slot[si];
   sl.pl = pl;
@@ -728,7 +733,7 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
     P.host_tail = std::chrono::duration<float, std::milli>(t1 - t0).count();
     P.entries = total;
     P.window_bits = pl.d.c;
-    P.windows = pl.d.W;
+    P.windows = pl.d.Wm;
     P.run_length = pl.K;
     P.chunk_len = pl.L;
     P.accumulate_sum += P.accumulate;
@@ -751,12 +756,17 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   const int si = 0;  // a lone MSM always uses slot 0 (the second workspace only for pipelining)
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   hipStream_t s = user_stream ? user_stream : c->slot[si].stream;
-  if ((rc = submit_msm(c, pl, d_points, d_scalars, si, s)) != MSM_OK) return rc;
+  BatchPtrs bp{}, bs{};
+  for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
+    bp.p[m] = d_points;
+    bs.p[m] = d_scalars;
+  }
+  if ((rc = submit_msm(c, pl, bp, bs, si, s)) != MSM_OK) return rc;
   return finish_msm(c, si, result);
 }
 
 // MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
-// and sort kernels leave most of the chip idle), so more of them run side by side; MSM_SLOTS
+// and sort kernels leave most of the chip idle), so several run side by side; MSM_SLOTS
 // overrides (1 = everything in order on one stream: clean per-kernel profiles).
 int pipeline_slots(size_t n) {
   static const int env = getenv("MSM_SLOTS") ? atoi(getenv("MSM_SLOTS")) : 0;
@@ -765,12 +775,25 @@ int pipeline_slots(size_t n) {
   return 3;  // measured best at 2^16..2^20 (4 streams contend for the hardware queues)
 }
 
+// MSMs per launch (batch) for the pipelined entries: the latency-bound kernels (reduction trees,
+// scans, small sorts) of two MSMs fill the machine together.  Measured on MI355X
+// (tools/batch_sweep.sh, ms per MSM, batch 1 -> 2): 2^16 0.218 -> 0.162, 2^17 0.273 -> 0.247,
+// 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136; 4 is no better than 2.
+// MSM_BATCH overrides (1..MSM_MAX_BATCH).
+uint32_t pipeline_batch(size_t n, size_t count) {
+  static const int env = getenv("MSM_BATCH") ? atoi(getenv("MSM_BATCH")) : 0;
+  uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH) : (n <= (1u << 20) ? 2u : 1u);
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
+}
+
 // `count` MSMs of n points each, pipelined over pipeline_slots(n) slots, each with its own stream
-// and workspace: later MSMs are enqueued before the host finishes MSM b, so the host tail (window
-// Horner) of one overlaps the device work of the next, and the MSMs' kernels may overlap on the
-// device (the latency-bound reduction of one beside another's sort and accumulation).  With a
-// caller-supplied stream everything runs in order on it.
-// Results go out affine (16 words each) or, with `projective`, as X|Y|T|Z partials (32 words).
+// and workspace, in launches of pipeline_batch MSMs (the last batch is padded by repeating its
+// last MSM, whose extra results are dropped): later batches are enqueued before the host
+// finishes batch j, so the host tail (window Horner) of one overlaps the device work of the
+// next, and the batches' kernels may overlap on the device (the latency-bound reduction of one
+// beside another's sort and accumulation).  With a caller-supplied stream everything runs in
+// order on it.  Results go out affine (16 words each) or, with `projective`, as X|Y|T|Z
+// partials (32 words).
 int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* d_scalars, size_t n, size_t count,
              const msm_opts* o, hipStream_t user_stream, uint32_t* out_be, bool projective) {
   auto emit = [&](const Pt& r, size_t b) {
@@ -783,33 +806,42 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
     for (size_t b = 0; b < count; b++) emit(pt_identity(), b);
     return MSM_OK;
   }
+  for (size_t b = 0; b < count; b++)
+    if (!d_points[b] || !d_scalars[b]) return MSM_ERR_INVALID_ARG;
+  const uint32_t nm = pipeline_batch(n, count);
+  const size_t nbatch = (count + nm - 1) / nm;
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl, count > 1);
+  int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm);
   if (rc != MSM_OK) return rc;
-  const int nslot = count > 1 ? (int)std::min<size_t>(count, (size_t)pipeline_slots(n)) : 1;
+  const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)pipeline_slots(n)) : 1;
   for (int si = 0; si < nslot; si++)
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };
-  // MSM b goes to slot b % nslot.  Its previous occupant, MSM b - nslot, is waited for and its
-  // window terms copied out just before; the host tail (window Horner) of MSM b - nslot runs
-  // after b is enqueued, so the device holds nslot MSMs while the host works (otherwise MSMs
-  // that finish together leave the device idle for a Horner each).
+  // Batch j goes to slot j % nslot.  Its previous occupant, batch j - nslot, is waited for and
+  // its window terms copied out just before; the host tail (window Horner) of batch j - nslot
+  // runs after j is enqueued, so the device holds nslot batches while the host works
+  // (otherwise batches that finish together leave the device idle for a Horner each).
   std::vector<uint32_t> terms;
   auto fail = [&](int code) {
     for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
     return code;
   };
-  for (size_t b = 0; b < count + nslot; b++) {
-    const bool have = b >= (size_t)nslot;
-    const size_t f = have ? b - nslot : 0;
+  for (size_t j = 0; j < nbatch + nslot; j++) {
+    const bool have = j >= (size_t)nslot;
+    const size_t f = have ? j - nslot : 0;
     if (have && (rc = finish_msm(c, (int)(f % nslot), nullptr, &terms)) != MSM_OK) return fail(rc);
-    if (b < count) {
-      const int si = (int)(b % nslot);
-      if (!d_points[b] || !d_scalars[b]) rc = MSM_ERR_INVALID_ARG;
-      else rc = submit_msm(c, pl, d_points[b], d_scalars[b], si, stream_of(si));
-      if (rc != MSM_OK) return fail(rc);
+    if (j < nbatch) {
+      BatchPtrs bp{}, bs{};
+      for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
+        const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
+        bp.p[m] = d_points[b];
+        bs.p[m] = d_scalars[b];
+      }
+      const int si = (int)(j % nslot);
+      if ((rc = submit_msm(c, pl, bp, bs, si, stream_of(si))) != MSM_OK) return fail(rc);
     }
-    if (have) emit(horner_tail(pl, terms.data()), f);
+    if (have)
+      for (uint32_t m = 0; m < nm && f * nm + m < count; m++) emit(horner_tail(pl, terms.data(), m), f * nm + m);
   }
   return MSM_OK;
 }

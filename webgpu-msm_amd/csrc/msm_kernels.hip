@@ -62,13 +62,16 @@ __device__ __forceinline__ fe load_fe(const uint32_t* src) {
 constexpr uint32_t PP_THREADS = MSM_PP_THREADS;
 __device__ __forceinline__ uint32_t pp_slot(uint32_t rec, uint32_t q) { return rec * 8 + (q ^ (rec & 7)); }
 
-extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(const uint32_t* __restrict__ wire,
+// blockIdx.y = MSM of the batch: its wire points come from wires.p[y], its records go to
+// pts[y n ..).
+extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchPtrs wires,
                                                                           uint32_t* __restrict__ pts, uint32_t n,
                                                                           uint32_t* __restrict__ err) {
   __shared__ uint4 st[PP_THREADS * 8];
   const uint32_t p0 = blockIdx.x * PP_THREADS;
   const uint32_t np = min(PP_THREADS, n - p0);
-  const uint4* src = reinterpret_cast<const uint4*>(wire) + (size_t)p0 * 8;
+  const uint4* src = reinterpret_cast<const uint4*>(wires.p[blockIdx.y]) + (size_t)p0 * 8;
+  pts += (size_t)blockIdx.y * n * PRE_WORDS;
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
     const uint32_t g = j * PP_THREADS + threadIdx.x;  // 16-B slot within the block's records
@@ -172,7 +175,7 @@ __device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32
 template <typename F>
 __device__ __forceinline__ void recode(uint32_t s[8], const MsmDims& d, F&& f) {
   uint32_t carry = 0;
-  for (uint32_t w = 0; w < d.W; w++) {
+  for (uint32_t w = 0; w < d.Wm; w++) {
     const uint32_t b = win_bits(d, w);
     const uint32_t half = 1u << (b - 1);
     const uint32_t v = (s[0] & ((1u << b) - 1u)) + carry;
@@ -263,12 +266,16 @@ constexpr uint32_t PS_R = MSM_PS_R;  // digits per lane (ch = PT_THREADS * PS_R)
 constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
 constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup (4 per lane)
 template <typename T>
-__global__ void __launch_bounds__(RC_THREADS) k_recode_hist(const uint32_t* __restrict__ scalars, MsmDims d,
+// blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its windows
+// [y Wm, (y+1) Wm).
+__global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_sets, MsmDims d,
                                                             T* __restrict__ digits, uint32_t* __restrict__ hist_rows) {
-  extern __shared__ uint32_t lds_hist[];  // [W][nbc]
+  extern __shared__ uint32_t lds_hist[];  // [Wm][nbc]
+  const uint32_t* __restrict__ scalars = scalar_sets.p[blockIdx.y];
   const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
   const uint32_t ck = lo / d.ch;
-  const uint32_t nh = d.W * d.nbc;
+  const uint32_t w0 = blockIdx.y * d.Wm;
+  const uint32_t nh = d.Wm * d.nbc;
   for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) lds_hist[b] = 0;
   __syncthreads();
   for (uint32_t i = lo + threadIdx.x; i < hi; i += RC_THREADS) {
@@ -281,7 +288,7 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(const uint32_t* __re
         code = mag | (digit < 0 ? DigitCode<T>::SIGN : 0u);
         atomicAdd(&lds_hist[w * d.nbc + (mag >> d.fb)], 1u);
       }
-      digits[(size_t)w * d.n + i] = (T)code;
+      digits[(size_t)(w0 + w) * d.n + i] = (T)code;
     });
   }
   __syncthreads();
@@ -289,7 +296,7 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(const uint32_t* __re
     const uint32_t v = lds_hist[b];
     if (v) {
       const uint32_t w = b / d.nbc, bin = b - w * d.nbc;
-      atomicAdd(&hist_rows[((size_t)w * d.nch + ck) * d.nbc + bin], v);
+      atomicAdd(&hist_rows[((size_t)(w0 + w) * d.nch + ck) * d.nbc + bin], v);
     }
   }
 }
@@ -396,6 +403,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
   uint32_t* lstart = dyn + d.nbc;
   uint32_t* gstart = dyn + 2 * d.nbc;
   const uint32_t w = blockIdx.y, ck = blockIdx.x;
+  const uint32_t pbase = (w / d.Wm) * d.n;  // first point record of this window's MSM
   const size_t row = ((size_t)w * d.nch + ck) * d.nbc;
   for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
     lcur[b] = hist_rows[row + b];
@@ -423,7 +431,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
       const uint32_t b = code[r] & DigitCode<T>::MAG;
       const uint32_t bin = b >> d.fb;
       const uint32_t p = atomicAdd(&lcur[bin], 1u);
-      st_entry[p] = (i << 1) | (code[r] >> DigitCode<T>::SHIFT);
+      st_entry[p] = ((pbase + i) << 1) | (code[r] >> DigitCode<T>::SHIFT);
       st_fine[p] = (uint16_t)(b & fmask);
       st_bin[p] = (uint16_t)bin;
     }
