@@ -316,6 +316,33 @@ def test_many_device_throughput_window(logn):
     assert M.compute_msm_device(d_pts, scs[0], n) == exps[0]  # lone MSM: c = 16
 
 
+def test_many_device_odd_count_and_bad_member():
+    # the pipelined entry launches MSMs two at a time: an odd count pads the last launch (its
+    # extra result is dropped), and a bad input anywhere in a launch fails the call
+    torch = pytest.importorskip("torch")
+    n = 3000
+    cases = []
+    for j in range(3):
+        pts = O.gen_points(n, k0=5 + j, step=1 + j)
+        ss = O.xorshift_scalars(n, seed=900 + j)
+        cases.append((torch.from_numpy(pts.view(np.int32)).cuda(),
+                      torch.from_numpy(O.ints_to_be_words(ss).view(np.int32)).cuda(),
+                      O.closed_form_msm([5 + j + (1 + j) * i for i in range(n)], ss)))
+    torch.cuda.synchronize()
+    out = M.compute_msm_many_device([c[0] for c in cases], [c[1] for c in cases], n)
+    assert out.shape == (3, 16)
+    for r, c in zip(out, cases):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == c[2]
+    bad = O.gen_points(n, k0=5, step=1)
+    bad[17, :8] = O.int_to_be_words(O.P + 3)  # x >= p
+    d_bad = torch.from_numpy(bad.view(np.int32)).cuda()
+    with pytest.raises(M.MsmError):
+        M.compute_msm_many_device([cases[0][0], d_bad, cases[2][0]], [c[1] for c in cases], n)
+    # the library recovers: the next call is correct
+    out = M.compute_msm_many_device([cases[1][0]] * 2, [cases[1][1]] * 2, n)
+    assert (O.be_words_to_int(out[1][:8]), O.be_words_to_int(out[1][8:])) == cases[1][2]
+
+
 def test_reference_format_test_case(tmp_path):
     # a case written in the reference's on-disk format (testCases.ts:34-52), z != 1 included
     from msm_amd import testdata as TD
