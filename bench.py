@@ -255,21 +255,25 @@ def main():
         nprof = max(1, int(prof["profiled"]))
         acc = float(prof["accumulate_sum"]) / nprof  # mean k_accumulate duration over the timed MSMs
         dev_total = float(prof["device_total_sum"]) / nprof
+        # the pipelined entry launches MSMs in batches (libmsm pipeline_batch): one timed
+        # k_accumulate launch covers `per_launch` MSMs, the isolated eager pass exactly one
+        per_launch = max(1, round(int(prof["entries"]) / max(1, int(phase_prof["entries"]))))
         algo_bytes = ALGO_BYTES_PER_POINT * m
-        achieved = algo_bytes / (acc * 1e-3) / 1e9
+        achieved = algo_bytes * per_launch / (acc * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
                 with open(args.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("n") == m:
-                    traffic = tj.get("accumulate_hbm_bytes_per_launch")
+                if tj.get("n") == m and tj.get("accumulate_hbm_bytes_per_msm"):
+                    traffic = tj["accumulate_hbm_bytes_per_msm"] * per_launch  # per timed launch
             except (OSError, ValueError):
                 traffic = None
         phases = {k: round(float(phase_prof[k]), 4) for k in (
             "prepare_points", "recode_count", "coarse_scan", "coarse_scatter", "fine_sort", "accumulate",
             "fixup", "bucket_reduce_1", "bucket_reduce_2", "readback", "device_total", "host_tail")}
-        entries = int(prof["entries"])
+        entries = int(prof["entries"])  # per timed launch (all MSMs of the launch)
+        entries_iso = int(phase_prof["entries"])  # one MSM
         # compute roofline: field multiplies per accumulation add = 7 (madd, ec.cuh)
         modmul_rate = entries * 7 / (acc * 1e-3) / 1e9
         line = {
@@ -295,17 +299,19 @@ def main():
                          "kernel_ms_timed": round(acc, 4),
                          "kernel_ms_isolated": round(acc_iso, 4),
                          "achieved_isolated": round(algo_bytes / (acc_iso * 1e-3) / 1e9, 2),
-                         "note": "achieved = algorithmic bytes (160 B x points per launch, SURVEY.md §8d) / mean "
-                                 "k_accumulate duration from hipEvents in the timed region (every 4th MSM "
-                                 "bracketed; the pipelined batch overlaps the other slot's kernels, so this is "
-                                 "the shared-GPU duration); *_isolated from one unoverlapped eager pass. traffic "
-                                 "= FETCH_SIZE + WRITE_SIZE per launch (profiles/traffic_latest.json). The "
-                                 "kernel is integer-VALU bound (~87% VALU busy): see compute_roofline"},
+                         "msms_per_launch": per_launch,
+                         "note": "achieved = algorithmic bytes (160 B x points x msms_per_launch, SURVEY.md "
+                                 "§8d) / mean k_accumulate launch duration from hipEvents in the timed region "
+                                 "(every 4th launch bracketed; the pipelined slots overlap each other's kernels, "
+                                 "so this is the shared-GPU duration); *_isolated from one unoverlapped eager "
+                                 "pass of one MSM. traffic = FETCH_SIZE + WRITE_SIZE per pipelined launch "
+                                 "(profiles/traffic_latest.json). The kernel is integer-VALU-issue bound: see "
+                                 "compute_roofline"},
             "compute_roofline": {"kernel": "k_accumulate", "achieved_gmodmul_s": round(modmul_rate, 1),
-                                 "achieved_isolated_gmodmul_s": round(entries * 7 / (acc_iso * 1e-3) / 1e9, 1),
+                                 "achieved_isolated_gmodmul_s": round(entries_iso * 7 / (acc_iso * 1e-3) / 1e9, 1),
                                  "peak_gmodmul_s": 167.7,
                                  "frac": round(modmul_rate / 167.7, 4),
-                                 "frac_isolated": round(entries * 7 / (acc_iso * 1e-3) / 1e9 / 167.7, 4),
+                                 "frac_isolated": round(entries_iso * 7 / (acc_iso * 1e-3) / 1e9 / 167.7, 4),
                                  "note": "7 field multiplies per accumulated entry (pt_madd); peak = measured fe_mul "
                                          "throughput, tools/ubench/fmul_bench.hip"},
             "phases_ms": phases,

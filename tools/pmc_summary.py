@@ -15,6 +15,7 @@ def short(name):
 
 def load(d):
     vals = defaultdict(lambda: defaultdict(list))
+    grids = defaultdict(dict)  # kernel -> counter -> [(dispatch grid size, summed value)]
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
@@ -23,6 +24,7 @@ def load(d):
                 v = float(row.get("Counter_Value", row.get("Counter-Value", "nan")))
                 disp = row.get("Dispatch_Id", row.get("Dispatch-Id"))
                 vals[k][c].append((disp, v))
+                grids[k][(c, disp)] = float(row.get("Grid_Size", "nan"))
     out = {}
     for k, cs in vals.items():
         out[k] = {}
@@ -32,6 +34,12 @@ def load(d):
                 per[disp] += v
             xs = list(per.values())
             out[k][c] = sum(xs) / len(xs)
+            # per unit of the smallest launch (one MSM): launches carrying a batch of MSMs have
+            # proportionally larger grids
+            g = {disp: grids[k][(c, disp)] for disp in per}
+            gmin = min(g.values())
+            units = sum(gv / gmin for gv in g.values())
+            out[k][c + "_per_unit"] = sum(xs) / units if units else float("nan")
     return out
 
 
@@ -56,17 +64,17 @@ def main():
     acc = s.get("k_accumulate")
     tr = None
     if acc and n:
-        fetch = acc.get("FETCH_SIZE", 0) * 1024
-        write = acc.get("WRITE_SIZE", 0) * 1024
+        fetch = acc.get("FETCH_SIZE_per_unit", 0) * 1024
+        write = acc.get("WRITE_SIZE_per_unit", 0) * 1024
         tr = {"n": n, "kernel": "k_accumulate",
-              "accumulate_fetch_bytes_per_launch": fetch,
-              "accumulate_write_bytes_per_launch": write,
-              "accumulate_hbm_bytes_per_launch": fetch + write,
-              "accumulate_fetch_x2_upper_bound": 2 * fetch,
-              "note": "FETCH_SIZE + WRITE_SIZE per launch (separate rocprofv3 --pmc passes). The guide's x2 "
-                      "FETCH correction is for 16-B/lane coalesced streaming reads; this kernel gathers one "
-                      "128-B point record per sorted entry, and raw FETCH_SIZE matches that known byte "
-                      "count (entries x 128 B) to within 1%, so raw is reported (x2 kept as an upper "
+              "accumulate_fetch_bytes_per_msm": fetch,
+              "accumulate_write_bytes_per_msm": write,
+              "accumulate_hbm_bytes_per_msm": fetch + write,
+              "accumulate_fetch_x2_upper_bound_per_msm": 2 * fetch,
+              "note": "FETCH_SIZE + WRITE_SIZE of k_accumulate per MSM (separate rocprofv3 --pmc passes; "
+                      "a launch carrying a batch of MSMs is counted per MSM by its grid size). Raw: the "
+                      "guide's x2 FETCH correction is for 16-B/lane coalesced streaming reads, while this "
+                      "kernel gathers 112 B of a 128-B point record per sorted entry (x2 kept as an upper "
                       "bound). Counted at the L2's fabric side: includes Infinity-Cache hits (the 128 MiB "
                       "point table stays resident in the 256 MiB Infinity Cache)."}
     print(json.dumps({"kernels": rows, "traffic": tr}, indent=1))
