@@ -9,10 +9,10 @@ HBM when the timed region starts: P_i = (i+1) G (G = the benchmark page's point,
 src/ui/AllBenchmarks.tsx:111-119), scalars = xorshift64 words mod p (SURVEY.md §8c spec), so
 the result is checked against the oracle-confirmed closed-form value.
 
-The K timed steps go through libmsm's pipelined entry (msm_compute_many_device): two slots, each
-with its own stream and workspace, so step i+1 runs on the device while the host finishes step
-i's window Horner.  `value` = wall time of the K steps / K (whole-job throughput); `latency_ms`
-is one unpipelined MSM end to end.
+The K timed steps go through libmsm's pipelined entry (msm_compute_many_device): MSMs launched
+two at a time, three launches in flight on their own streams and workspaces, so the device runs
+later MSMs while the host finishes earlier ones' window Horner.  `value` = wall time of the K
+steps / K (whole-job throughput); `latency_ms` is one unpipelined MSM end to end.
 
 With N > 1 ranks every rank takes a contiguous 1/N of the points (no data-path collective),
 computes its K partial points (pipelined the same way), the K x 128 B partials are all-gathered

@@ -753,7 +753,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl);
   if (rc != MSM_OK) return rc;
-  const int si = 0;  // a lone MSM always uses slot 0 (the second workspace only for pipelining)
+  const int si = 0;  // a lone MSM always uses slot 0 (the other workspaces only for pipelining)
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   hipStream_t s = user_stream ? user_stream : c->slot[si].stream;
   BatchPtrs bp{}, bs{};
