@@ -343,6 +343,24 @@ def test_many_device_odd_count_and_bad_member():
     assert (O.be_words_to_int(out[1][:8]), O.be_words_to_int(out[1][8:])) == cases[1][2]
 
 
+def test_unpacked_partition_entries():
+    # coarse-binned entries carry their fine key in one u32 while the launch's points fit in
+    # 2^(31 - fb) (msm_dev.h MsmDims::packed); c = 20 (fb = 11) with two MSMs of 2^19 + 3 points
+    # per launch does not fit, so the two-array path runs
+    torch = pytest.importorskip("torch")
+    n = (1 << 19) + 3
+    d_pts = torch.from_numpy(O.gen_points(n, k0=2, step=3).view(np.int32)).cuda()
+    scs, exps = [], []
+    for j in range(2):
+        ss = O.xorshift_scalars(n, seed=1300 + j)
+        scs.append(torch.from_numpy(O.ints_to_be_words(ss).view(np.int32)).cuda())
+        exps.append(O.closed_form_msm(range(2, 2 + 3 * n, 3), ss))
+    torch.cuda.synchronize()
+    out = M.compute_msm_many_device([d_pts] * 2, scs, n, window_size=20)
+    for r, exp in zip(out, exps):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == exp
+
+
 def test_reference_format_test_case(tmp_path):
     # a case written in the reference's on-disk format (testCases.ts:34-52), z != 1 included
     from msm_amd import testdata as TD

@@ -33,6 +33,8 @@ struct MsmDims {
   uint32_t nbins;  // W * nbc
   uint32_t ch;     // digits per partition workgroup (one window chunk)
   uint32_t nch;    // chunks per window = ceil(n / ch)
+  uint32_t packed; // coarse-binned entries carry their fine key: (entry << fb) | fine in one u32
+                   // (when nm n <= 2^(31 - fb)); else a separate u16 array holds the fine keys
 };
 
 

@@ -280,6 +280,7 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   while (nbc < d.B && (d.B / nbc) > FS_MAXF) nbc <<= 1;
   d.nbc = nbc;
   d.fb = ilog2(d.B / nbc);
+  d.packed = ((uint64_t)nm * n) <= (1ull << (31 - d.fb)) ? 1u : 0u;
   d.nbins = d.W * d.nbc;
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);

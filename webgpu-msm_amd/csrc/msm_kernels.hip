@@ -441,8 +441,12 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
   for (uint32_t j = threadIdx.x; j < m; j += PT_THREADS) {
     const uint32_t bin = st_bin[j];
     const uint32_t dst = gstart[bin] + (j - lstart[bin]);
-    part_entry[dst] = st_entry[j];
-    part_fine[dst] = st_fine[j];
+    if (d.packed) {
+      part_entry[dst] = (st_entry[j] << d.fb) | st_fine[j];
+    } else {
+      part_entry[dst] = st_entry[j];
+      part_fine[dst] = st_fine[j];
+    }
   }
 }
 
@@ -457,6 +461,24 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
 // and one placement cursor per bucket -- and its entries are placed by k_big_place, whose
 // workgroups share the bin tile by tile.  Counting collapses runs of equal keys per lane before
 // touching LDS, so a bin that is one giant bucket costs one atomic per lane, not per entry.
+
+// One coarse-binned entry: its fine key (bucket within the bin) and the sorted-list entry
+// (idx << 1 | sign), from the packed word or the two arrays (MsmDims::packed).
+__device__ __forceinline__ uint32_t part_fine_at(const uint32_t* __restrict__ pe, const uint16_t* __restrict__ pf,
+                                                 const MsmDims& d, uint32_t i) {
+  return d.packed ? pe[i] & ((1u << d.fb) - 1u) : (uint32_t)pf[i];
+}
+__device__ __forceinline__ void part_load(const uint32_t* __restrict__ pe, const uint16_t* __restrict__ pf,
+                                          const MsmDims& d, uint32_t i, uint32_t& fine, uint32_t& entry) {
+  const uint32_t v = pe[i];
+  if (d.packed) {
+    fine = v & ((1u << d.fb) - 1u);
+    entry = v >> d.fb;
+  } else {
+    fine = pf[i];
+    entry = v;
+  }
+}
 
 __device__ __forceinline__ void count_runs(uint32_t* cnt, uint32_t& last, uint32_t& run, uint32_t key) {
   if (key == last) {
@@ -492,11 +514,27 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
   const bool staged = m <= FS_CAP;
   uint32_t fk[FS_R], en[FS_R];
   if (staged) {
+    // every load issued before any is used; the packed/unpacked choice is uniform
+    if (d.packed) {
+      const uint32_t fmask = (1u << d.fb) - 1u;
 #pragma unroll
-    for (uint32_t r = 0; r < FS_R; r++) {
-      const uint32_t e = r * FS_THREADS + threadIdx.x;
-      fk[r] = e < m ? part_fine[base + e] : 0xffffu;
-      en[r] = e < m ? part_entry[base + e] : 0u;
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const uint32_t e = r * FS_THREADS + threadIdx.x;
+        en[r] = e < m ? part_entry[base + e] : 0u;
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const uint32_t e = r * FS_THREADS + threadIdx.x;
+        fk[r] = e < m ? en[r] & fmask : 0xffffu;
+        en[r] >>= d.fb;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const uint32_t e = r * FS_THREADS + threadIdx.x;
+        fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+        en[r] = e < m ? part_entry[base + e] : 0u;
+      }
     }
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++)
@@ -509,7 +547,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
         const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
-        fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+        fk[r] = e < m ? part_fine_at(part_entry, part_fine, d, base + e) : 0xffffu;
       }
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++)
@@ -548,8 +586,14 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
         const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
-        fk[r] = e < m ? part_fine[base + e] : 0xffffu;
-        en[r] = e < m ? part_entry[base + e] : 0u;
+        if (d.packed) {
+          const uint32_t v = e < m ? part_entry[base + e] : 0u;
+          fk[r] = e < m ? v & ((1u << d.fb) - 1u) : 0xffffu;
+          en[r] = v >> d.fb;
+        } else {
+          fk[r] = e < m ? part_fine[base + e] : 0xffffu;
+          en[r] = e < m ? part_entry[base + e] : 0u;
+        }
       }
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++)
@@ -592,7 +636,8 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_big_place(const uint3
     for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
     __syncthreads();
     uint32_t last = 0, run = 0;
-    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS) count_runs(cnt, last, run, part_fine[base + t0 + e]);
+    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS)
+      count_runs(cnt, last, run, part_fine_at(part_entry, part_fine, d, base + t0 + e));
     if (run) atomicAdd(&cnt[last], run);
     __syncthreads();
     for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) {
@@ -601,8 +646,9 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_big_place(const uint3
     }
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS) {
-      const uint32_t f = part_fine[base + t0 + e];
-      sorted_entry[atomicAdd(&cnt[f], 1u)] = part_entry[base + t0 + e];
+      uint32_t f, en;
+      part_load(part_entry, part_fine, d, base + t0 + e, f, en);
+      sorted_entry[atomicAdd(&cnt[f], 1u)] = en;
     }
     __syncthreads();
   }
