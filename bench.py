@@ -44,6 +44,13 @@ EXPECTED = {
               6067849550923149820308908062064106891655248540786717479864185323992998585544),
     1 << 16: (6511033747840878550891912519839400034267046616019718682893517787635890491406,
               8324633492142170543892201760308347298775556742917471112781391167726746210774),
+    # same spec, closed form (tests/golden/gen_golden.py `closed_form` rows)
+    1 << 17: (7214186375342905655836331870791036211588304483548747369939589357052012718094,
+              1086641463988251823483984585140441696641479012220914034026585318064758089041),
+    1 << 18: (2518859951884126800468133890192010299375092073488953920640060520721235089022,
+              4561108318479168802718042014814226601666750618193314344765242268012430256975),
+    1 << 19: (2494697504588773044226079827451750530847598622692644691585706184092107244181,
+              7646105785862097369609424364128279727770382720292428742097192424906359768460),
 }
 
 

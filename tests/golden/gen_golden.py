@@ -43,6 +43,17 @@ def survey_rows():
     return rows
 
 
+def closed_form_rows():
+    # the bench's other sizes (same spec; the closed form is pinned by the survey rows above)
+    rows = []
+    for logn in (17, 18, 19):
+        n = 1 << logn
+        x, y = O.closed_form_msm(range(1, n + 1), O.xorshift_scalars(n))
+        rows.append({"name": f"closed_form_2^{logn}", "n": n, "k0": 1, "step": 1, "scalars": "xorshift64",
+                     "seed": hex(O.XORSHIFT_SEED), "x": str(x), "y": str(y), "source": "closed form"})
+    return rows
+
+
 def small_case(name, ks, ss, check_c=True):
     x, y = O.closed_form_msm(ks, ss)
     if check_c and len(ks) <= 2048:
@@ -84,6 +95,7 @@ def main():
         "G": [str(O.G[0]), str(O.G[1])],
         "small": cases,
         "survey": survey_rows(),
+        "closed_form": closed_form_rows(),
     }
     with open(os.path.join(HERE, "msm_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)

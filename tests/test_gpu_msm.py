@@ -185,6 +185,19 @@ def test_survey_rows(golden, logn):
     assert M.compute_msm_wire(pts, sc, window_size=16) == exp  # BASELINE config 2 (c = 16)
 
 
+@pytest.mark.parametrize("logn", [17, 18, 19])
+def test_closed_form_rows_pipelined(golden, logn):
+    # the bench's other sizes, through the pipelined entry (two MSMs per launch, throughput window)
+    torch = pytest.importorskip("torch")
+    row = {r["n"]: r for r in golden["msm"]["closed_form"]}[1 << logn]
+    n = row["n"]
+    d_pts = torch.from_numpy(M.gen_points(n).view(np.int32)).cuda()
+    d_sc = torch.from_numpy(M.gen_scalars(n).view(np.int32)).cuda()
+    out = M.compute_msm_many_device([d_pts] * 3, [d_sc] * 3, n)
+    for r in out:
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == (int(row["x"]), int(row["y"]))
+
+
 def test_survey_2_20(golden):
     row = {r["n"]: r for r in golden["msm"]["survey"]}[1 << 20]
     pts = O.gen_points(1 << 20)

@@ -97,6 +97,14 @@ def test_survey_rows_closed_form(golden):
     assert r["x"] == r["aleo_wasm_confirmed_x"]
 
 
+def test_closed_form_rows_match_c_oracle(golden):
+    # the 2^17 bench row: closed form == the C restatement of the reference's Pippenger
+    r = {r["n"]: r for r in golden["msm"]["closed_form"]}[1 << 17]
+    pts = O.gen_points(1 << 17)
+    sc = O.xorshift_scalars_np(1 << 17)
+    assert O.msm(pts, sc, window=12, threads=8) == (int(r["x"]), int(r["y"]))
+
+
 def test_c_oracle_matches_survey_2_12(golden):
     r = {r["n"]: r for r in golden["msm"]["survey"]}[1 << 12]
     pts = O.gen_points(1 << 12)
