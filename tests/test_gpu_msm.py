@@ -185,11 +185,12 @@ def test_survey_rows(golden, logn):
     assert M.compute_msm_wire(pts, sc, window_size=16) == exp  # BASELINE config 2 (c = 16)
 
 
-@pytest.mark.parametrize("logn", [17, 18, 19])
+@pytest.mark.parametrize("logn", [17, 18, 19, 20])
 def test_closed_form_rows_pipelined(golden, logn):
-    # the bench's other sizes, through the pipelined entry (two MSMs per launch, throughput window)
+    # the bench's sizes through the pipelined entry (two MSMs per launch, throughput window; at
+    # 2^20 also the 16-bucket reduction chunks of the pipelined plan)
     torch = pytest.importorskip("torch")
-    row = {r["n"]: r for r in golden["msm"]["closed_form"]}[1 << logn]
+    row = {r["n"]: r for r in golden["msm"]["closed_form"] + golden["msm"]["survey"]}[1 << logn]
     n = row["n"]
     d_pts = torch.from_numpy(M.gen_points(n).view(np.int32)).cuda()
     d_sc = torch.from_numpy(M.gen_scalars(n).view(np.int32)).cuda()

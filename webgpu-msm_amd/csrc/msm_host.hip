@@ -292,7 +292,11 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   pl->K = (o && o->run_length) ? o->run_length : kauto;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
   static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
-  pl->L = l_env == 4 ? 4u : 8u;  // L = 4 measured no faster at any size (tools/l_sweep.sh)
+  // Buckets per k_bucket_reduce_1 lane.  L = 16 halves k_bucket_reduce_2's bit-term work but
+  // doubles the running-sum chain: a throughput win only for the wide pipelined windows (2^20:
+  // -1.5% per MSM; single-MSM latency +50 us at 2^18-2^19).  tools/l_sweep.sh; MSM_RED_L overrides.
+  pl->L = (l_env == 4 || l_env == 8 || (l_env == 16 && d.B >= 32)) ? l_env
+          : (pipelined && d.B >= (1u << 15)) ? 16u : 8u;
   pl->lgL = ilog2(pl->L);
   pl->nchunks = d.B / pl->L;
   // every k_bucket_reduce_2 workgroup sums at most nchunks/2 points (the R_k terms' size)
@@ -430,7 +434,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
                      w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
   mark(PH_FIXUP);
-  hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : k_bucket_reduce_1<8>,
+  hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : pl.L == 16 ? k_bucket_reduce_1<16> : k_bucket_reduce_1<8>,
                      dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s, w.buckets.as<uint32_t>(),
                      w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(),
                      w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());

@@ -1156,17 +1156,15 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
       __syncthreads();
     }
   }
-  if (threadIdx.x == 0) {
-    acc = load_pt_lds(sh[0]);
-    uint32_t* o = out_host + (size_t)blockIdx.x * 32;
-    fe c4[4] = {fe_to_host_mont(acc.X), fe_to_host_mont(acc.Y), fe_to_host_mont(acc.T), fe_to_host_mont(acc.Z)};
+  if (threadIdx.x < 4) {  // one lane per coordinate (X, Y, T, Z): the conversions run side by side
+    const uint32_t q = threadIdx.x;
+    uint32_t* o = out_host + (size_t)blockIdx.x * 32 + 8 * q;
     uint32_t wd[8];
+    fe_to_words_le(fe_to_host_mont(load_fe_lds(&sh[0][q * NL])), wd);
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      fe_to_words_le(c4[q], wd);
-#pragma unroll
-      for (int k = 0; k < 8; k++) o[8 * q + k] = wd[k];
-    }
+    for (int k = 0; k < 8; k++) o[k] = wd[k];
+  }
+  if (threadIdx.x == 0) {
     if (blockIdx.x == 0) {
       const size_t tail = (size_t)gridDim.x * 32;
       out_host[tail] = *err;
