@@ -199,6 +199,25 @@ def test_closed_form_rows_pipelined(golden, logn):
         assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == (int(row["x"]), int(row["y"]))
 
 
+def test_many_device_skewed_2_20():
+    # the pipelined 2^20 plan (16-bucket reduction chunks) under bucket skew: giant buckets drive
+    # the chain / lead / cross-workgroup joins that feed k_bucket_reduce_1
+    torch = pytest.importorskip("torch")
+    n = 1 << 20
+    d_pts = torch.from_numpy(M.gen_points(n).view(np.int32)).cuda()
+    s = 0x0DEADBEEF1234567_89ABCDEF0FEDCBA9_8765432112345678_9ABCDEF011223344 % O.P
+    vals = [s, 3 * s % O.P, (1 << 190) + 12345]
+    eq = np.tile(O.ints_to_be_words([s]), (n, 1))
+    few = np.tile(O.ints_to_be_words(vals), (n // 3 + 1, 1))[:n]
+    exp_eq = O.scalar_mul(O.G, s * (n * (n + 1) // 2) % O.R_ORDER)
+    exp_few = O.scalar_mul(O.G, sum(v * sum(range(j + 1, n + 1, 3)) for j, v in enumerate(vals)) % O.R_ORDER)
+    d_eq = torch.from_numpy(eq.view(np.int32)).cuda()
+    d_few = torch.from_numpy(np.ascontiguousarray(few).view(np.int32)).cuda()
+    out = M.compute_msm_many_device([d_pts] * 4, [d_eq, d_few, d_few, d_eq], n)
+    for r, exp in zip(out, (exp_eq, exp_few, exp_few, exp_eq)):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == exp
+
+
 def test_survey_2_20(golden):
     row = {r["n"]: r for r in golden["msm"]["survey"]}[1 << 20]
     pts = O.gen_points(1 << 20)

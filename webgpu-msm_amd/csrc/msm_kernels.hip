@@ -1042,9 +1042,15 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
                                                          const uint32_t* __restrict__ lead_val,
                                                          uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
   const uint32_t nchunks = d.B / RL;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= d.W * nchunks) return;
-  const uint32_t w = g / nchunks, c = g % nchunks;
+  const uint32_t gd = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gd >= d.W * nchunks) return;
+  // Dispatch order: every MSM's main windows first, the overflow windows (empty for canonical
+  // scalars: their lanes return at once) last.  The real work is then exactly 1 (L = 16) or 2
+  // (L = 8) waves per SIMD at 2^20 instead of spilling a tail round onto a few CUs.
+  const uint32_t wd = gd / nchunks, c = gd % nchunks;
+  const uint32_t nmain = d.nm * (d.Wm - 1);
+  const uint32_t w = wd < nmain ? (wd / (d.Wm - 1)) * d.Wm + wd % (d.Wm - 1) : (wd - nmain) * d.Wm + d.Wm - 1;
+  const uint32_t g = w * nchunks + c;
   const uint32_t key0 = w * d.B + c * RL;
   // bucket metadata up front (independent loads): which buckets are non-empty, and which left
   // their accumulation workgroup and need the continuation from lead_val
