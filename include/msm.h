@@ -33,11 +33,18 @@ extern "C" {
 #define MSM_ERR_NO_DEVICE (-6)          /* no gfx950 device visible: there is no CPU fallback */
 #define MSM_ERR_OOM (-7)                /* device allocation failed                           */
 
+/* hip_stream argument of the *_device entries: order after the null (legacy default) stream,
+ * e.g. torch's default stream (whose handle is 0, i.e. indistinguishable from "no stream"). */
+#define MSM_STREAM_NULL ((void*)1)
+
+/* msm_opts.flags */
+#define MSM_FLAG_SERIAL 1u /* pipelined entries: one launch in flight at a time (no overlap)     */
+
 typedef struct msm_opts {
   uint32_t window_bits; /* 0 = auto (msm_best_window); else 4..20. Replaces ?windowSize (submission.ts:29-33) */
   uint32_t run_length;  /* sorted-list entries per accumulation lane; 0 = auto                     */
-  int32_t device;       /* HIP device ordinal, -1 = the calling thread's current device           */
-  uint32_t flags;       /* reserved, 0                                                            */
+  int32_t device;       /* HIP device ordinal (a gfx950 one), -1 = the calling thread's current device */
+  uint32_t flags;       /* MSM_FLAG_* (0 = defaults)                                              */
 } msm_opts;
 
 /* Per-phase device times (ms) of the most recent MSM on the calling thread's device when
@@ -49,9 +56,12 @@ typedef struct msm_profile_t {
   float host_tail;    /* host Horner + affine conversion (wall) */
   uint64_t entries;   /* nonzero digits sorted (= accumulation adds) */
   uint32_t window_bits, windows, run_length, chunk_len;
-  double accumulate_sum; /* sum of `accumulate` over every MSM profiled since msm_set_profiling */
+  double accumulate_sum; /* sum of `accumulate` over every launch profiled since msm_set_profiling */
   double device_total_sum;
-  uint32_t profiled;     /* number of MSMs in those sums */
+  uint32_t profiled;     /* number of launches in those sums */
+  uint32_t msms_per_launch; /* MSMs one launch (and one k_accumulate) covers */
+  double accumulate_union_sum; /* wall time with >= 1 k_accumulate in flight, summed over the calls
+                                  since msm_set_profiling (launches in flight may overlap) */
 } msm_profile_t;
 
 /* Library lifetime.  msm_init replaces the wasm init()/initThreadPool (submission.ts:89-93);
@@ -65,12 +75,18 @@ const char* msm_strerror(int code);
 uint32_t msm_best_window(size_t n);
 
 /* compute_msm: host-resident inputs, result on the host.  n = 0 gives the identity (0, 1),
- * like the oracle's empty `Address.msm`. */
+ * like the oracle's empty `Address.msm`.  The inputs are uploaded on a copy stream, scalars first
+ * (the bucket sort starts on them) and points in 8 MiB pieces, each prepared as it lands
+ * (generalises the reference's staging ring, gpu.ts:146-155 / 244-271).  The caller keeps
+ * ownership of the arrays; they are not read after the call returns. */
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                 uint32_t out_xy_be[16]);
 
 /* Same with inputs already in device memory (device pointers, wire layout).  `hip_stream` may be
- * NULL (library stream) or a hipStream_t to order against the caller's work. */
+ * NULL or a hipStream_t: the library's streams then wait for the work enqueued on it so far (the
+ * inputs it produces), and the call returns when the result is on the host.  With NULL the
+ * caller must have completed the inputs' producers (e.g. torch.cuda.synchronize()).  The same
+ * holds for every *_device entry below. */
 int msm_compute_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
                        void* hip_stream, uint32_t out_xy_be[16]);
 
@@ -102,6 +118,30 @@ int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const ui
                                     size_t n, size_t count, const msm_opts* opts, void* hip_stream,
                                     uint32_t* out_xyzt_be);
 
+/* Prover batch: `count` independent MSMs over ONE base vector (d_points_be, [n][32]) with their own
+ * scalar vectors d_scalars_be[b] ([n][8] each); results [count][16].  The base vector is prepared
+ * once per call (k_prepare_points) and every MSM reads its records; otherwise as
+ * msm_compute_many_device.  BASELINE configs[4] (64 x 2^18). */
+int msm_compute_shared_device(const uint32_t* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
+                              size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
+
+/* Host-resident batches (the streaming API of SURVEY.md §8f2).  msm_compute_many: `count`
+ * independent MSMs, per-MSM host arrays; msm_compute_shared: one host base vector, per-MSM host
+ * scalar vectors.  Inputs are uploaded on a copy stream into the in-flight launch slots while the
+ * other slots compute (the base vector of msm_compute_shared once, piece by piece, prepared as it
+ * lands).  Results [count][16]. */
+int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
+                     const msm_opts* opts, uint32_t* out_xy_be);
+int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
+                       const msm_opts* opts, uint32_t* out_xy_be);
+
+/* The reference's CPU-only path (cpuWorkRatio = 1: submission.ts:96-115 -> msm_end_to_end,
+ * lib.rs:24-44, 106-121) as the library's own multithreaded host Pippenger: signed c-bit digits,
+ * 7M mixed adds into per-thread bucket tables.  window_bits 0 = auto, n_threads <= 0 = all
+ * hardware threads.  An explicit entry, never a fallback for the GPU entries. */
+int msm_compute_cpu(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, uint32_t window_bits,
+                    int n_threads, uint32_t out_xy_be[16]);
+
 /* point_add_affine (lib.rs:240-253): affine a + b -> affine, 16 words each. */
 int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]);
 
@@ -119,8 +159,9 @@ int msm_gen_points(const uint32_t g_xy_be[16], uint64_t k0, uint64_t step, size_
 int msm_gen_scalars(uint64_t seed, size_t n, uint32_t* scalars_be);
 
 /* Profiling.  enable = 0: off; 1: hipEvents between every phase (launches go eagerly, no graph
- * replay); 2: k_accumulate and the device total only (events between graph replays, so the
- * timed path is the production one).  msm_last_profile reports the calling thread's device. */
+ * replay); 2: k_accumulate's duration and the device total of every launch (the production path:
+ * k_accumulate always runs between two events).  msm_last_profile reports the calling thread's
+ * device. */
 int msm_set_profiling(int enable);
 int msm_last_profile(msm_profile_t* out);
 

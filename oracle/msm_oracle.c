@@ -310,16 +310,16 @@ int oracle_split(uint32_t c, const uint32_t* scalars_be, size_t n, uint32_t* out
 }
 
 typedef struct {
-  const uint32_t* digits; /* this window's n digits */
+  const uint32_t* digits; /* this window's digits of the job's points */
   const ept* points;
   size_t n;
   uint32_t c;
   ept result;
 } win_job;
 
-/* bucket_cpu (lib.rs:24-44) + bucket_sum_cpu (lib.rs:46-56) for one window */
-static void* window_job(void* arg) {
-  win_job* j = (win_job*)arg;
+/* bucket_cpu (lib.rs:24-44) + bucket_sum_cpu (lib.rs:46-56) for one window over a slice of the
+ * points (the window's sum is the sum of its slices' sums: the bucket sum is linear) */
+static void window_job(win_job* j) {
   size_t nb = (size_t)1 << j->c;
   ept* bucket = (ept*)malloc(nb * sizeof(ept));
   for (size_t b = 0; b < nb; b++) bucket[b] = p_zero();
@@ -338,10 +338,29 @@ static void* window_job(void* arg) {
   }
   free(bucket);
   j->result = sum;
-  return NULL;
 }
 
-/* msm_end_to_end (lib.rs:106-121): returns 0, or -3 if a coordinate >= p (bytes.rs:19 panics). */
+typedef struct {
+  win_job* jobs;
+  uint32_t njobs;
+  uint32_t next;
+  pthread_mutex_t mu;
+} job_queue;
+
+static void* job_worker(void* arg) {
+  job_queue* q = (job_queue*)arg;
+  for (;;) {
+    pthread_mutex_lock(&q->mu);
+    uint32_t k = q->next++;
+    pthread_mutex_unlock(&q->mu);
+    if (k >= q->njobs) return NULL;
+    window_job(&q->jobs[k]);
+  }
+}
+
+/* msm_end_to_end (lib.rs:106-121): returns 0, or -3 if a coordinate >= p (bytes.rs:19 panics).
+ * The reference's rayon parallelism is over windows; here the jobs are (window, point slice)
+ * pairs on `threads` workers, so every host core stays busy whatever the window count. */
 int oracle_msm(uint32_t c, const uint32_t* scalars_be, const uint32_t* points_be, size_t n, int threads,
                uint32_t* out16) {
   init_consts();
@@ -362,20 +381,36 @@ int oracle_msm(uint32_t c, const uint32_t* scalars_be, const uint32_t* points_be
   }
   uint32_t* split = (uint32_t*)malloc(((size_t)nw * n + 1) * sizeof(uint32_t));
   oracle_split(c, scalars_be, n, split);
+  if (threads < 1) threads = 1;
+  /* slices per window: at least two jobs per worker, at least 4096 points per slice */
+  uint32_t ns = (uint32_t)((2 * (size_t)threads + nw - 1) / nw);
+  if (ns > n / 4096) ns = (uint32_t)(n / 4096);
+  if (ns < 1) ns = 1;
+  job_queue q;
+  q.njobs = nw * ns;
+  q.next = 0;
+  q.jobs = (win_job*)calloc(q.njobs, sizeof(win_job));
+  pthread_mutex_init(&q.mu, NULL);
+  for (uint32_t w = 0; w < nw; w++)
+    for (uint32_t sl = 0; sl < ns; sl++) {
+      size_t lo = n * sl / ns, hi = n * (sl + 1) / ns;
+      win_job* j = &q.jobs[w * ns + sl];
+      j->digits = split + (size_t)w * n + lo;
+      j->points = pts + lo;
+      j->n = hi - lo;
+      j->c = c;
+    }
+  uint32_t nth = (uint32_t)threads < q.njobs ? (uint32_t)threads : q.njobs;
+  pthread_t* th = (pthread_t*)malloc(nth * sizeof(pthread_t));
+  for (uint32_t t = 0; t < nth; t++) pthread_create(&th[t], NULL, job_worker, &q);
+  for (uint32_t t = 0; t < nth; t++) pthread_join(th[t], NULL);
+  pthread_mutex_destroy(&q.mu);
   win_job* jobs = (win_job*)calloc(nw, sizeof(win_job));
   for (uint32_t w = 0; w < nw; w++) {
-    jobs[w].digits = split + (size_t)w * n;
-    jobs[w].points = pts;
-    jobs[w].n = n;
-    jobs[w].c = c;
+    jobs[w].result = p_zero();
+    for (uint32_t sl = 0; sl < ns; sl++) jobs[w].result = p_add(&jobs[w].result, &q.jobs[w * ns + sl].result);
   }
-  if (threads < 1) threads = 1;
-  pthread_t* th = (pthread_t*)malloc(nw * sizeof(pthread_t));
-  for (uint32_t w0 = 0; w0 < nw; w0 += (uint32_t)threads) {
-    uint32_t w1 = w0 + (uint32_t)threads < nw ? w0 + (uint32_t)threads : nw;
-    for (uint32_t w = w0; w < w1; w++) pthread_create(&th[w], NULL, window_job, &jobs[w]);
-    for (uint32_t w = w0; w < w1; w++) pthread_join(th[w], NULL);
-  }
+  free(q.jobs);
   /* reduce_last (lib.rs:88-104): windows MSB-first, sum = 2^c sum + W */
   ept sum = p_zero();
   for (uint32_t w = 0; w < nw; w++) {

@@ -1,0 +1,52 @@
+"""Generate tests/golden/bench_expected.json: the expected MSM results bench.py checks every timed
+step against (test infrastructure; bench.py only reads the JSON).
+
+Inputs follow the survey's spec: P_i = (i+1) G with G the benchmark page's point
+(AllBenchmarks.tsx:111-119), scalars from xorshift64(13,7,17) seeded XORSHIFT_SEED + j, 4 words
+each (first most significant), reduced mod p.  Expected value = ((sum s_i (i+1)) mod r) G, the
+closed form the survey verified against the Aleo-wasm oracle at 2^12, 2^16 and 2^20 (seed j = 0;
+this script re-asserts those rows).
+
+    python tests/golden/gen_bench_expected.py        (~1 min, pure Python)
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+ROWS = [(1 << lg, j) for lg in (16, 17, 18, 19, 20) for j in range(4)]
+ROWS += [(1 << 18, j) for j in range(4, 64)]  # the prover batch (BASELINE configs[4]): 64 seeds
+ROWS += [(1 << 16, j) for j in range(4, 64)]  # the same batch shape at 2^16 (quick runs)
+
+
+def expected(n: int, j: int):
+    ss = O.xorshift_scalars(n, O.XORSHIFT_SEED + j)
+    acc = 0
+    for i, s in enumerate(ss):
+        acc += (i + 1) * s
+    return O.scalar_mul(O.G, acc % O.R_ORDER)
+
+
+def main():
+    with open(os.path.join(HERE, "msm_vectors.json")) as f:
+        survey = {r["n"]: (int(r["x"]), int(r["y"])) for r in json.load(f)["survey"]}
+    out = {"spec": "P_i=(i+1)G (AllBenchmarks.tsx:111-119); scalars xorshift64(13,7,17) seed "
+                   "0x9e3779b97f4a7c15 + j, 4 words MSB first, mod p; value = ((sum s_i (i+1)) mod r) G",
+           "rows": {}}
+    for n, j in ROWS:
+        x, y = expected(n, j)
+        if j == 0 and n in survey:
+            assert (x, y) == survey[n], f"closed form disagrees with the survey-recorded oracle at n={n}"
+        out["rows"][f"{n}:{j}"] = [str(x), str(y)]
+        print(n, j, flush=True)
+    with open(os.path.join(HERE, "bench_expected.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+"""GPU parity of libmsm's launch paths added for host-resident inputs, shared base vectors
+(prover batch), caller-stream ordering, serial launches and the captured-graph cache.
+
+Every expected value is the closed form sum s_i (k_i G) = ((sum s_i k_i) mod r) G, which the
+survey pinned to the Aleo-wasm oracle at 2^12..2^20 (tests/golden/msm_vectors.json); comparisons
+are bit-exact.
+"""
+import numpy as np
+import pytest
+
+import msm_amd as M
+from _closed_form import as_xy, closed_form
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).cuda()
+
+
+def test_host_entry_ragged_pieces():
+    # msm_compute uploads points in 65536-point pieces, each prepared as it lands: three pieces,
+    # the last one partial and not a multiple of the preparation workgroup
+    n = 2 * 65536 + 77
+    pts = M.gen_points(n, k0=5, step=3)
+    sc = M.gen_scalars(n, seed=31)
+    exp = closed_form(5, 3, sc)
+    assert M.compute_msm_wire(pts, sc) == exp
+    assert M.compute_msm_wire(pts, sc, window_size=13) == exp
+    # an exact multiple of the piece
+    n2 = 65536
+    assert M.compute_msm_wire(pts[:n2], sc[:n2]) == closed_form(5, 3, sc[:n2])
+
+
+def test_host_many_distinct():
+    cases = []
+    for j, n in enumerate((3000, 3000, 3000, 3000, 3000)):
+        pts = M.gen_points(n, k0=2 + j, step=1 + j)
+        sc = M.gen_scalars(n, seed=400 + j)
+        cases.append((pts, sc, closed_form(2 + j, 1 + j, sc)))
+    order = [0, 1, 2, 3, 4, 1, 0]
+    out = M.compute_msm_many([cases[i][0] for i in order], [cases[i][1] for i in order], 3000)
+    for r, i in zip(out, order):
+        assert as_xy(r) == cases[i][2], i
+
+
+def test_host_many_large_pieces():
+    n = (1 << 17) + 5
+    pts = [M.gen_points(n, k0=1 + j, step=2) for j in range(3)]
+    scs = [M.gen_scalars(n, seed=500 + j) for j in range(3)]
+    out = M.compute_msm_many(pts, scs, n)
+    for j in range(3):
+        assert as_xy(out[j]) == closed_form(1 + j, 2, scs[j])
+
+
+def test_shared_base_vector_host_and_device():
+    # the prover-batch entries: one base vector, prepared once per call, many scalar vectors
+    n = 20000
+    pts = M.gen_points(n, k0=7, step=5)
+    scs = [M.gen_scalars(n, seed=600 + j) for j in range(7)]
+    exps = [closed_form(7, 5, s) for s in scs]
+    out = M.compute_msm_shared(pts, scs)
+    for r, e in zip(out, exps):
+        assert as_xy(r) == e
+    d_pts = _dev(pts)
+    d_scs = [_dev(s) for s in scs]
+    out = M.compute_msm_shared_device(d_pts, d_scs, n)
+    for r, e in zip(out, exps):
+        assert as_xy(r) == e
+    # mixed with the distinct-base entry on the same slots (different point-record buffers,
+    # different captured segments) and a single MSM in between
+    out = M.compute_msm_many_device([d_pts] * 3, d_scs[:3], n)
+    for r, e in zip(out, exps[:3]):
+        assert as_xy(r) == e
+    assert M.compute_msm_device(d_pts, d_scs[4], n) == exps[4]
+    out = M.compute_msm_shared_device(d_pts, d_scs[::-1], n)
+    for r, e in zip(out, exps[::-1]):
+        assert as_xy(r) == e
+    # a count of one, and a bad point fails the whole call
+    out = M.compute_msm_shared_device(d_pts, d_scs[:1], n)
+    assert as_xy(out[0]) == exps[0]
+    bad = pts.copy()
+    bad[123, 8:16] = 0xFFFFFFFF  # y >= p
+    with pytest.raises(M.MsmError) as e:
+        M.compute_msm_shared(bad, scs[:3])
+    assert e.value.code == -3
+    out = M.compute_msm_shared(pts, scs[:2])  # recovers
+    assert as_xy(out[1]) == exps[1]
+
+
+@pytest.mark.parametrize("n", [1 << 18])
+def test_shared_prover_batch_shape(n):
+    # BASELINE configs[4] per rank: MSMs of 2^18 points over one base vector, distinct seeds
+    d_pts = _dev(M.gen_points(n))
+    scs = [M.gen_scalars(n, seed=M.XORSHIFT_SEED + b) for b in range(8)]
+    out = M.compute_msm_shared_device(d_pts, [_dev(s) for s in scs], n)
+    for b in range(8):
+        assert as_xy(out[b]) == closed_form(1, 1, scs[b]), b
+
+
+def test_graph_cache_keyed_on_whole_plan():
+    # above 2^20 a lone MSM and a pipelined pair both use one MSM per launch and
+    # c = 16 but different reduction chunk lengths (L = 8 vs 16); a replayed graph of the other
+    # plan would read the window terms at the wrong offsets.  Alternate the two, twice.
+    n = (1 << 20) + 1
+    pts = M.gen_points(n)
+    scs = [M.gen_scalars(n, seed=700 + j) for j in range(2)]
+    exps = [closed_form(1, 1, s) for s in scs]
+    d_pts = _dev(pts)
+    d_scs = [_dev(s) for s in scs]
+    for _ in range(2):
+        assert M.compute_msm_device(d_pts, d_scs[0], n) == exps[0]
+        out = M.compute_msm_many_device([d_pts, d_pts], d_scs, n)
+        assert [as_xy(r) for r in out] == exps
+
+
+def test_caller_stream_ordering():
+    # inputs produced by torch kernels still in flight on a side stream: passing that stream
+    # (or leaving the default: torch's current stream) orders libmsm after them
+    import torch
+
+    n = 1 << 16
+    pts = M.gen_points(n, k0=3, step=2)
+    sc = M.gen_scalars(n, seed=801)
+    exp = closed_form(3, 2, sc)
+    host_p = torch.from_numpy(pts.view(np.int32)).pin_memory()
+    host_s = torch.from_numpy(sc.view(np.int32)).pin_memory()
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(side):
+            d_p = torch.zeros_like(host_p, device="cuda")
+            d_s = torch.zeros_like(host_s, device="cuda")
+            # a long chain of small kernels before the real data lands
+            for _ in range(200):
+                d_p.add_(1)
+            d_p.copy_(host_p, non_blocking=True)
+            d_s.copy_(host_s, non_blocking=True)
+            assert M.compute_msm_device(d_p, d_s, n) == exp  # torch's current stream = side
+        with torch.cuda.stream(side):
+            d_s.zero_()
+            d_s.copy_(host_s, non_blocking=True)
+        assert M.compute_msm_device(d_p, d_s, n, stream=side.cuda_stream) == exp
+        with torch.cuda.stream(side):
+            d_s.zero_()
+            d_s.copy_(host_s, non_blocking=True)
+        out = M.compute_msm_many_device([d_p] * 2, [d_s] * 2, n, stream=side.cuda_stream)
+        assert [as_xy(r) for r in out] == [exp, exp]
+    # the default (null) stream too
+    d_p = torch.zeros_like(host_p, device="cuda")
+    d_s = torch.zeros_like(host_s, device="cuda")
+    d_p.copy_(host_p, non_blocking=True)
+    d_s.copy_(host_s, non_blocking=True)
+    assert M.compute_msm_device(d_p, d_s, n) == exp
+
+
+def test_serial_flag_and_profile():
+    n = 1 << 16
+    d_pts = _dev(M.gen_points(n))
+    scs = [M.gen_scalars(n, seed=900 + j) for j in range(5)]
+    exps = [closed_form(1, 1, s) for s in scs]
+    M.set_profiling(2)
+    try:
+        out = M.compute_msm_many_device([d_pts] * 5, [_dev(s) for s in scs], n, flags=M.MSM_FLAG_SERIAL)
+        prof = M.last_profile()
+    finally:
+        M.set_profiling(False)
+    assert [as_xy(r) for r in out] == exps
+    # every launch is timed (k_accumulate between two events): 5 MSMs in launches of 2
+    assert prof["profiled"] == 3 and prof["msms_per_launch"] == 2
+    assert 0 < prof["accumulate_sum"] / prof["profiled"] < 50.0

@@ -11,7 +11,8 @@ arithmetic on the limb maxima) and asserts:
     subtraction needed);
   * fe_sub / fe_neg never produce a negative limb (K8P dominates the subtrahend limb-wise).
 
-It mirrors the kernels by hand: when a formula in ec.cuh changes, change it here too.
+It mirrors the kernels by hand; test_mirrored_sources_unchanged pins a digest of every mirrored
+function body, so an edit to fp29.cuh / ec.cuh fails until the model here is re-reviewed.
 """
 P = 8444461749428370424248824938781546531375899335154063827935233455917409239041
 NL, LB = 9, 29
@@ -157,3 +158,56 @@ def test_model_matches_header_constants():
     assert value_of(K8P29) == 8 * P
     assert all(k >= MASK for k in K8P29[:8])
     assert P29 == [1, 277610496, 66, 351141280, 452990362, 110046747, 358187729, 198395284, 1223525]
+
+
+# --- the proof above mirrors these device functions by hand.  Their normalised source text is
+# pinned here, so editing any of them fails this test until the mirrored formulas (and this
+# table) are re-reviewed.  Regenerate a digest with _body_digest(<file>, <name>).
+import hashlib  # noqa: E402
+import os  # noqa: E402
+import re  # noqa: E402
+
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "webgpu-msm_amd", "csrc")
+REVIEWED = {
+    ("fp29.cuh", "mad64"): "b50540a0d8a64ede",
+    ("fp29.cuh", "seeded"): "d5de263bcd90d0e8",
+    ("fp29.cuh", "fe_mul"): "e89342f9ea9e59ca",
+    ("fp29.cuh", "fe_norm"): "37b756e7bd4474d2",
+    ("fp29.cuh", "fe_add"): "d14b6a137a6ff34d",
+    ("fp29.cuh", "fe_add_n"): "bdf7dd24032e38f7",
+    ("fp29.cuh", "fe_dbl_n"): "07019b3ba4e2775f",
+    ("fp29.cuh", "fe_sub"): "ea72835f159885cc",
+    ("fp29.cuh", "fe_sub_u"): "3dba987a0530b5b5",
+    ("fp29.cuh", "fe_neg"): "a754b1a94a6b8415",
+    ("fp29.cuh", "P29"): "b4babf5a3c9d7331",
+    ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
+    ("ec.cuh", "pt_madd"): "bca5cd1691b5dc73",
+    ("ec.cuh", "pt_add"): "f730177c97e49172",
+    ("ec.cuh", "pt_dbl"): "784353f9934ef437",
+    ("ec.cuh", "pre_neg_if"): "a318c90204dc7c80",
+    ("ec.cuh", "pt_add_quad"): "917a5a92a88578ac",
+}
+
+
+def _body(fname, name):
+    src = open(os.path.join(_CSRC, fname)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    m = re.search(r"[^\n;{}]*\b" + re.escape(name) + r"\b\s*(\[[^\]]*\])?\s*(\([^)]*\))?\s*(=\s*)?\{", src)
+    assert m, f"{name} not found in {fname}"
+    i, depth = m.end() - 1, 0
+    for j in range(i, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[j], 0)
+        if depth == 0:
+            return " ".join((src[m.start():j + 1]).split())
+    raise AssertionError(f"unbalanced braces after {name} in {fname}")
+
+
+def _body_digest(fname, name):
+    return hashlib.sha256(_body(fname, name).encode()).hexdigest()[:16]
+
+
+def test_mirrored_sources_unchanged():
+    changed = {f"{f}:{n}": _body_digest(f, n) for (f, n), d in REVIEWED.items() if _body_digest(f, n) != d}
+    assert not changed, ("device code mirrored by this proof changed -- re-check the formulas above, then update "
+                         f"REVIEWED with: {changed}")

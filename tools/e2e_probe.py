@@ -1,0 +1,42 @@
+"""msm_compute end to end from host arrays (upload + MSM + result), for timeline profiling:
+
+    python tools/e2e_probe.py [--n 1048576] [--runs 6]
+    rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/e2e -- python3 tools/e2e_probe.py
+
+Prints one JSON line: per-run wall times (ms) and whether each result matched the closed form.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "webgpu-msm_amd")):
+    sys.path.insert(0, p)
+
+import msm_amd as M  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--runs", type=int, default=6)
+    args = ap.parse_args()
+    with open(os.path.join(ROOT, "tests", "golden", "bench_expected.json")) as f:
+        row = json.load(f)["rows"].get(f"{args.n}:0")
+    exp = (int(row[0]), int(row[1])) if row else None
+    pts = M.gen_points(args.n)
+    sc = M.gen_scalars(args.n)
+    times, ok = [], []
+    for _ in range(args.runs):
+        t0 = time.perf_counter()
+        r = M.compute_msm_wire(pts, sc)
+        times.append(round((time.perf_counter() - t0) * 1e3, 3))
+        ok.append(exp is None or r == exp)
+    print(json.dumps({"n": args.n, "e2e_ms": times, "correct": all(ok),
+                      "pin": os.environ.get("MSM_H2D_PIN", "0")}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+"""Static instruction mix of k_accumulate's hot loop (the one-entry mixed-add block) and the VALU
+issue cycles it demands per wave-iteration on gfx950.
+
+    python tools/isa_mix.py [--out profiles/r2_isa_mix.json]
+
+Compiles libmsm's device code with --save-temps into a scratch directory, takes the basic block
+of k_accumulate holding the most v_mad_u64_u32 (one pt_madd per wave-iteration), and prices it
+with the issue costs measured by tools/ubench/isa_rates.hip (profiles/r2_isa_rates.json): a
+SIMD-32 issues a 32-bit VALU wave64 instruction in 2 cycles and a 64-bit one (v_mad_u64_u32,
+64-bit shifts/adds/moves) in 4.  bench.py turns cycles_per_iteration into the ISA roofline:
+frac_isa = (entries / 64) * cycles_per_iteration / (k_accumulate seconds * SIMDs * clock).
+"""
+import argparse
+import collections
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "webgpu-msm_amd", "csrc", "msm_host.hip")
+VALU64 = {"v_mad_u64_u32", "v_mad_i64_i32", "v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_mov_b64",
+          "v_add_u64", "v_ashrrev_i64", "v_fma_f64"}
+
+
+def asm_text(tmp):
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared", "--save-temps",
+           "-Xarch_host", "-mbmi2", "-Xarch_host", "-madx", "-o", os.path.join(tmp, "lib.so"), SRC]
+    subprocess.run(cmd, cwd=tmp, check=True, capture_output=True)
+    with open(os.path.join(tmp, "msm_host-hip-amdgcn-amd-amdhsa-gfx950.s")) as f:
+        return f.read()
+
+
+def blocks_of(asm, func):
+    lines = asm.splitlines()
+    start = next(i for i, l in enumerate(lines) if l.startswith(func + ":"))
+    out, loops, cur = {}, set(), None
+    for l in lines[start:]:
+        if l.startswith(".Lfunc_end"):
+            break
+        m = re.match(r"^(\.LBB\w+|" + func + r"):", l)
+        if m:
+            cur = m.group(1)
+            out[cur] = []
+            if "Loop" in l:  # the assembler's "in Loop: Header=..." / "Loop Header" annotation
+                loops.add(cur)
+            continue
+        s = l.strip()
+        if cur and s and not s.startswith((";", ".")):
+            out[cur].append(s.split()[0])
+    return out, loops
+
+
+def base(op):
+    return re.sub(r"_e(32|64)$", "", op)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_isa_mix.json"))
+    ap.add_argument("--func", default="k_accumulate")
+    args = ap.parse_args()
+    with tempfile.TemporaryDirectory() as tmp:
+        blocks, loops = blocks_of(asm_text(tmp), args.func)
+    # the loop block with the most multiplies: one entry's pt_madd per wave-iteration
+    name, ins = max(((k, v) for k, v in blocks.items() if k in loops),
+                    key=lambda kv: sum(1 for o in kv[1] if o == "v_mad_u64_u32"))
+    cnt = collections.Counter(base(o) for o in ins)
+    v64 = sum(c for o, c in cnt.items() if o in VALU64)
+    v32 = sum(c for o, c in cnt.items() if o.startswith("v_") and o not in VALU64)
+    cycles = 4 * v64 + 2 * v32
+    res = {"kernel": args.func, "block": name, "instructions": len(ins), "valu64": v64, "valu32": v32,
+           "v_mad_u64_u32": cnt["v_mad_u64_u32"],
+           "vmem_loads": sum(c for o, c in cnt.items() if o.startswith(("global_load", "buffer_load"))),
+           "cycles_per_iteration": cycles,
+           "cycle_model": "gfx950 SIMD-32: 2 cycles per 32-bit VALU wave64 instruction, 4 per 64-bit one "
+                          "(v_mad_u64_u32, 64-bit shifts/adds/moves); profiles/r2_isa_rates.json",
+           "mix": dict(cnt.most_common())}
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "mix"}))
+
+
+if __name__ == "__main__":
+    main()

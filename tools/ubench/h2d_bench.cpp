@@ -1,0 +1,189 @@
+// Host->device upload microbenchmark (MI355X box): picks the host-input staging strategy of
+// msm_compute.  Prints one JSON line per measurement.
+//   hipcc -O2 -std=c++17 --offload-arch=gfx950 -o h2d_bench h2d_bench.cpp -lpthread
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+using clk = std::chrono::steady_clock;
+static double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); }
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e = (x);                                                    \
+    if (e != hipSuccess) {                                                 \
+      fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e));        \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+static void par_copy(char* dst, const char* src, size_t bytes, int th) {
+  if (th <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> ts;
+  size_t per = (bytes + th - 1) / th;
+  per = (per + 4095) & ~size_t(4095);
+  for (int t = 0; t < th; t++) {
+    size_t lo = std::min(bytes, t * per), hi = std::min(bytes, lo + per);
+    ts.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+// persistent pool: workers spin on a generation counter while a call is active
+struct Pool {
+  int n;
+  std::vector<std::thread> ts;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<int> done{0};
+  std::atomic<bool> quit{false};
+  char* dst = nullptr;
+  const char* src = nullptr;
+  size_t bytes = 0;
+  explicit Pool(int n_) : n(n_) {
+    for (int i = 1; i < n; i++)
+      ts.emplace_back([this, i] {
+        uint64_t seen = 0;
+        while (!quit.load()) {
+          uint64_t g = gen.load(std::memory_order_acquire);
+          if (g == seen) {
+            __builtin_ia32_pause();
+            continue;
+          }
+          seen = g;
+          part(i);
+          done.fetch_add(1, std::memory_order_release);
+        }
+      });
+  }
+  void part(int i) {
+    size_t per = ((bytes + n - 1) / n + 4095) & ~size_t(4095);
+    size_t lo = std::min(bytes, i * per), hi = std::min(bytes, lo + per);
+    if (hi > lo) memcpy(dst + lo, src + lo, hi - lo);
+  }
+  void copy(char* d, const char* s, size_t b) {
+    dst = d;
+    src = s;
+    bytes = b;
+    done.store(0);
+    gen.fetch_add(1, std::memory_order_release);
+    part(0);
+    while (done.load(std::memory_order_acquire) < n - 1) __builtin_ia32_pause();
+  }
+  ~Pool() {
+    quit = true;
+    for (auto& t : ts) t.join();
+  }
+};
+
+int main(int argc, char** argv) {
+  const size_t MB = 1 << 20;
+  const size_t total = (argc > 1 ? atoi(argv[1]) : 160) * MB;
+  char* host = (char*)aligned_alloc(4096, total);
+  for (size_t i = 0; i < total; i += 8) *(uint64_t*)(host + i) = i * 0x9E3779B97F4A7C15ull;
+  void* dev;
+  CK(hipMalloc(&dev, total));
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  auto rep = [&](const char* what, double ms, const char* extra = "") {
+    printf("{\"what\": \"%s\", \"ms\": %.3f, \"GBps\": %.1f%s}\n", what, ms, total / ms / 1e6, extra);
+    fflush(stdout);
+  };
+  // pageable
+  for (int r = 0; r < 3; r++) {
+    auto t0 = clk::now();
+    CK(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    if (r == 2) rep("pageable_memcpy", ms_since(t0));
+  }
+  // pinned source
+  char* pin;
+  auto tp = clk::now();
+  CK(hipHostMalloc((void**)&pin, total, hipHostMallocDefault));
+  rep("hipHostMalloc_alloc", ms_since(tp));
+  memcpy(pin, host, total);
+  for (int r = 0; r < 3; r++) {
+    auto t0 = clk::now();
+    CK(hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    if (r == 2) rep("pinned_memcpy", ms_since(t0));
+  }
+  // register in place
+  for (int r = 0; r < 2; r++) {
+    auto t0 = clk::now();
+    CK(hipHostRegister(host, total, hipHostRegisterDefault));
+    double reg = ms_since(t0);
+    auto t1 = clk::now();
+    CK(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    double cp = ms_since(t1);
+    auto t2 = clk::now();
+    CK(hipHostUnregister(host));
+    double unreg = ms_since(t2);
+    char ex[128];
+    snprintf(ex, sizeof ex, ", \"register_ms\": %.3f, \"copy_ms\": %.3f, \"unregister_ms\": %.3f", reg, cp, unreg);
+    if (r == 1) rep("host_register_copy", reg + cp + unreg, ex);
+  }
+  // host memcpy pageable -> pinned, T threads
+  for (int th : {1, 4, 8, 16, 32}) {
+    Pool pool(th);
+    pool.copy(pin, host, total);
+    auto t0 = clk::now();
+    pool.copy(pin, host, total);
+    char ex[64];
+    snprintf(ex, sizeof ex, ", \"threads\": %d", th);
+    rep("host_memcpy_to_pinned", ms_since(t0), ex);
+  }
+  // staged ring: pool memcpy into pinned chunk k, async DMA, overlap
+  for (int th : {8, 16}) {
+    Pool pool(th);
+    for (size_t chunk : {2 * MB, 4 * MB, 8 * MB, 16 * MB}) {
+      const int NST = 4;
+      hipEvent_t ev[NST];
+      for (int k = 0; k < NST; k++) CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+      double best = 1e9;
+      for (int r = 0; r < 3; r++) {
+        auto t0 = clk::now();
+        int k = 0;
+        bool used[NST] = {};
+        for (size_t off = 0; off < total; off += chunk, k = (k + 1) % NST) {
+          size_t b = std::min(chunk, total - off);
+          if (used[k]) CK(hipEventSynchronize(ev[k]));
+          pool.copy(pin + k * chunk, host + off, b);
+          CK(hipMemcpyAsync((char*)dev + off, pin + k * chunk, b, hipMemcpyHostToDevice, s));
+          CK(hipEventRecord(ev[k], s));
+          used[k] = true;
+        }
+        CK(hipStreamSynchronize(s));
+        best = std::min(best, ms_since(t0));
+      }
+      char ex[96];
+      snprintf(ex, sizeof ex, ", \"threads\": %d, \"chunk_MiB\": %zu", th, chunk / MB);
+      rep("staged_ring", best, ex);
+      for (int k = 0; k < NST; k++) hipEventDestroy(ev[k]);
+    }
+  }
+  // pinned source, chunked DMA (the pinned-input fast path)
+  for (size_t chunk : {4 * MB, 16 * MB}) {
+    auto t0 = clk::now();
+    for (size_t off = 0; off < total; off += chunk)
+      CK(hipMemcpyAsync((char*)dev + off, pin + off, std::min(chunk, total - off), hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    char ex[64];
+    snprintf(ex, sizeof ex, ", \"chunk_MiB\": %zu", chunk / MB);
+    rep("pinned_chunked", ms_since(t0), ex);
+  }
+  hipHostFree(pin);
+  hipFree(dev);
+  free(host);
+  return 0;
+}

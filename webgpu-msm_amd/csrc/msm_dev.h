@@ -35,6 +35,8 @@ struct MsmDims {
   uint32_t nch;    // chunks per window = ceil(n / ch)
   uint32_t packed; // coarse-binned entries carry their fine key: (entry << fb) | fine in one u32
                    // (when nm n <= 2^(31 - fb)); else a separate u16 array holds the fine keys
+  uint32_t shared; // every MSM of the batch uses ONE base vector (prover batch): entries index
+                   // point records [0, n) instead of [m n, (m+1) n)
 };
 
 

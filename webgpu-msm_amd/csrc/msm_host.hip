@@ -3,23 +3,28 @@
 // The reference's host orchestration this replaces:
 //   compute_msm            src/submission/submission.ts:25-157   -> msm_compute / msm_compute_device
 //   getBestWindowSize      submission.ts:18-23                    -> msm_best_window
-//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_fixup
+//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_lead_scan
+//     (its staging ring, gpu.ts:146-155 / 244-271)                -> upload_points (chunked, overlapped)
 //   split_dynamic          msm-wasm/src/lib.rs:196-202            -> msm_split (host) / k_recode_* (device)
 //   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1/2
 //   reduce_last            lib.rs:88-104                          -> horner_tail (host)
 //   point_add_affine       lib.rs:240-253                         -> msm_point_add_affine
+//   msm_end_to_end         lib.rs:24-44, 106-121                  -> msm_compute_cpu (msm_cpu.h)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <vector>
 
 #include "../../include/msm.h"
 #include "hostfield.h"
+#include "msm_cpu.h"
 #include "msm_util.h"
 #include "msm_kernels.hip"
 
@@ -52,14 +57,16 @@ enum Phase {
   PH_COUNT
 };
 
-uint64_t g_alloc_gen = 0;  // bumped on every (re)allocation: captured graphs hold raw pointers
+// Bumped on every (re)allocation anywhere: captured graphs hold raw pointers, so a graph is
+// replayed only while the generation it was captured under is current.
+std::atomic<uint64_t> g_alloc_gen{0};
 
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return MSM_OK;
-    g_alloc_gen++;
+    g_alloc_gen.fetch_add(1);
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -87,7 +94,7 @@ struct HostBuf {
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return MSM_OK;
-    g_alloc_gen++;
+    g_alloc_gen.fetch_add(1);
     if (p) hipHostFree(p);
     p = nullptr;
     cap = 0;
@@ -120,82 +127,120 @@ struct Plan {
   size_t runs_max;
 };
 
+// Every field that shapes a launch (grids, buffer offsets, the h_out layout): a captured graph is
+// replayed only for an identical plan.
+bool plan_eq(const Plan& a, const Plan& b) {
+  const MsmDims &x = a.d, &y = b.d;
+  return x.n == y.n && x.c == y.c && x.B == y.B && x.W == y.W && x.Wm == y.Wm && x.nm == y.nm && x.q == y.q &&
+         x.nhi == y.nhi && x.fb == y.fb && x.nbc == y.nbc && x.nbins == y.nbins && x.ch == y.ch && x.nch == y.nch &&
+         x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L && a.lgL == b.lgL &&
+         a.nchunks == b.nchunks && a.nv == b.nv && a.nterms == b.nterms && a.Mmax == b.Mmax &&
+         a.runs_max == b.runs_max;
+}
+
 // Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
 struct Workspace {
   Buf pts, err, digits, hist_rows, rel, colsum, bin_base;
   Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets, big_tiles, cursor;
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
+  Buf wire_pts, wire_sc;  // device copies of host-resident inputs (msm_compute*, host entries)
   void release() {
     Buf* bufs[] = {&pts, &err, &digits, &hist_rows, &rel, &colsum, &bin_base, &part_entry, &part_fine,
                    &sorted_entry, &bucket_start, &run_key, &buckets, &big_tiles, &cursor, &lead_val, &lead_open, &cross_key,
-                   &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T};
+                   &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T, &wire_pts, &wire_sc};
     for (Buf* b : bufs) b->release();
   }
 };
 
-// One in-flight MSM: its own stream, device workspace, result buffer, captured graphs and events.
-// Several slots let msm_compute_many_device keep MSMs b+1.. on the device while MSM b is still
-// there (the latency-bound tails of one overlap the others' kernels) and while the host
-// finishes MSM b (window Horner).
+// Launch-sequence parts.  PREP: wire points -> precomputed records; SORT: scalar recoding and the
+// bucket sort; ACC: bucket accumulation; POST: skew joins and the bucket reduction.
+constexpr int PART_PREP = 1, PART_SORT = 2, PART_ACC = 4, PART_POST = 8, PART_ALL = 15;
+
+// One captured graph of a slot: a contiguous part of the launch sequence for one plan.
+struct Segment {
+  Plan pl{};
+  int parts = 0;
+  const uint32_t* pts_buf = nullptr;  // the point-record buffer the captured kernels use
+  bool acc_events = false;            // event-record nodes around k_accumulate
+  uint64_t gen = 0;
+  uint64_t used = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  // the kernel nodes that take the MSM's input buffers: repointed per launch
+  hipGraphNode_t n_prep = nullptr, n_recode = nullptr;
+  hipKernelNodeParams p_prep{}, p_recode{};
+  BatchPtrs in_pts{}, in_sc{};
+  void drop() {
+    if (exec) hipGraphExecDestroy(exec);
+    if (graph) hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    n_prep = n_recode = nullptr;
+    parts = 0;
+  }
+};
+constexpr int NSEG = 6;
+
+// One in-flight launch (one or a batch of MSMs): its own stream, device workspace, result buffer,
+// captured graph segments and events.  Several slots let the pipelined entries keep launches
+// j+1.. on the device while launch j is still there (the latency-bound tails of one overlap the
+// others' kernels) and while the host finishes launch j (window Horner).
 struct Slot {
   hipStream_t stream = nullptr;
   Workspace ws;
   HostBuf h_out;  // k_bucket_reduce_2 writes the window terms, err and total here
   void* h_out_dev = nullptr;
-  struct GraphKey {
-    size_t n;
-    uint32_t c, K, nm;
-    int prof;
-    uint64_t gen;
-    bool operator==(const GraphKey& o) const {
-      return n == o.n && c == o.c && K == o.K && nm == o.nm && prof == o.prof && gen == o.gen;
-    }
-  } gkey{};
-  hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
-  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};  // whole MSM, or pre / - / post
-  // the two kernel nodes (in graph[0]) that take the MSM's input buffers: repointed per launch
-  hipGraphNode_t n_prep = nullptr, n_recode = nullptr;
-  hipKernelNodeParams p_prep{}, p_recode{};
-  BatchPtrs g_pts{}, g_sc{};  // inputs the instantiated graph currently reads
+  Segment seg[NSEG];
+  uint64_t seg_clock = 0;
   hipEvent_t ev_start = nullptr, ev_acc0 = nullptr, ev_acc1 = nullptr, ev_end = nullptr, ev_done = nullptr;
+  hipEvent_t ev_in = nullptr;  // inputs of the slot's next launch are in place (uploads, caller's stream)
   Plan pl{};
-  bool bracketed = false;
+  bool acc_timed = false;
 };
-constexpr int NSLOT = 4;  // at most this many MSMs in flight (one HIP stream each)
-constexpr uint32_t PROF_EVERY = 4;
+constexpr int NSLOT = 4;      // at most this many launches in flight (one HIP stream each)
+constexpr int NCHUNK_EV = 8;  // events marking uploaded point chunks
 
 struct DevCtx {
   int device = -1;
   int n_cu = 256;
   std::mutex mu;
-  Buf wire_points, wire_scalars;  // staging for host-resident inputs (msm_compute)
   Slot slot[NSLOT];
-  uint32_t prof_seq = 0;
+  hipStream_t copy_stream = nullptr;  // host->device uploads (overlap the slots' kernels)
+  hipEvent_t ev_chunk[NCHUNK_EV] = {};
+  hipEvent_t ev_user = nullptr;  // recorded on a caller's stream: the library's streams wait on it
+  hipEvent_t ev_shared = nullptr;
+  Buf shared_pts;  // point records of a shared base vector (msm_compute_shared*)
   hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
-  int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate only (graph-friendly)
-  // The launch sequence of each slot is captured once into HIP graphs and replayed: one
-  // hipGraphLaunch instead of ~16 enqueues per MSM.
+  int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate + device total per launch
+  // The launch sequence of each slot is captured into HIP graphs and replayed: one
+  // hipGraphLaunch instead of ~14 enqueues per launch.
   bool graphs_ok = true;
+  bool graph_events_ok = true;  // event-record nodes can be added to captured graphs here
+  hipEvent_t ev_base = nullptr;  // per-call time origin of the accumulation intervals (profiling 2)
+  std::vector<std::pair<float, float>> acc_ivals;
   msm_profile_t last{};
 };
 
 std::mutex g_mu;
-std::vector<DevCtx*> g_ctx;
+std::vector<DevCtx*> g_ctx;   // indexed by HIP ordinal
+std::vector<int> g_gfx950;    // HIP ordinals of the gfx950 devices
+int g_nhip = -1;              // HIP devices visible (any architecture)
 int g_profiling = 0;
-int g_ndev = -1;
 
 int probe_devices() {
-  if (g_ndev >= 0) return g_ndev;
+  if (g_nhip >= 0) return (int)g_gfx950.size();
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
-  int good = 0;
+  g_nhip = n;
   for (int i = 0; i < n; i++) {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) good++;
+    if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+      g_gfx950.push_back(i);
   }
-  g_ndev = good == n ? n : good;
-  return g_ndev;
+  return (int)g_gfx950.size();
 }
+
+bool is_gfx950(int device) { return std::find(g_gfx950.begin(), g_gfx950.end(), device) != g_gfx950.end(); }
 
 int get_ctx(int device, DevCtx** out) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -203,8 +248,10 @@ int get_ctx(int device, DevCtx** out) {
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) return MSM_ERR_HIP;
   }
-  if (device >= g_ndev) return MSM_ERR_INVALID_ARG;
-  if ((int)g_ctx.size() < g_ndev) g_ctx.resize(g_ndev, nullptr);
+  // opts.device is a HIP ordinal; only gfx950 ordinals are accepted (a mixed node keeps its
+  // numbering)
+  if (device >= g_nhip || !is_gfx950(device)) return MSM_ERR_INVALID_ARG;
+  if ((int)g_ctx.size() < g_nhip) g_ctx.resize(g_nhip, nullptr);
   if (!g_ctx[device]) {
     DevCtx* c = new DevCtx();
     c->device = device;
@@ -214,20 +261,25 @@ int get_ctx(int device, DevCtx** out) {
       delete c;
       return MSM_ERR_HIP;
     }
-    for (Slot& sl : c->slot) {
-      if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        hipSetDevice(prev);
-        return MSM_ERR_HIP;
-      }
+    bool ok = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
+    for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
+      delete c;
+      hipSetDevice(prev);
+      return MSM_ERR_HIP;
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
+    for (int i = 0; i < NCHUNK_EV; i++) hipEventCreateWithFlags(&c->ev_chunk[i], hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_user, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_shared, hipEventDisableTiming);
+    hipEventCreate(&c->ev_base);
     for (Slot& sl : c->slot) {
       hipEventCreate(&sl.ev_start);
       hipEventCreate(&sl.ev_acc0);
       hipEventCreate(&sl.ev_acc1);
       hipEventCreate(&sl.ev_end);
       hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
+      hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming);
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -235,7 +287,6 @@ int get_ctx(int device, DevCtx** out) {
     hipSetDevice(prev);
     g_ctx[device] = c;
   }
-  g_ctx[device]->profiling = g_profiling;
   *out = g_ctx[device];
   return MSM_OK;
 }
@@ -257,11 +308,14 @@ uint32_t pipelined_window(size_t n) {
   return msm_best_window(n);
 }
 
-int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1) {
+int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1,
+              bool shared = false) {
+  (void)n_cu;
+  *pl = Plan{};
   uint32_t c = (o && o->window_bits) ? o->window_bits : pipelined ? pipelined_window(n) : msm_best_window(n);
   if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
   if (n >= (1ull << 30)) return MSM_ERR_INVALID_ARG;
-  MsmDims d;
+  MsmDims d{};
   d.n = (uint32_t)n;
   d.c = c;
   // balanced main windows of at most c bits over MAIN_BITS, plus the overflow window
@@ -280,7 +334,9 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   while (nbc < d.B && (d.B / nbc) > FS_MAXF) nbc <<= 1;
   d.nbc = nbc;
   d.fb = ilog2(d.B / nbc);
-  d.packed = ((uint64_t)nm * n) <= (1ull << (31 - d.fb)) ? 1u : 0u;
+  d.shared = shared ? 1u : 0u;
+  const uint64_t npts = shared ? n : (uint64_t)nm * n;  // point records the entries index
+  d.packed = npts <= (1ull << (31 - d.fb)) ? 1u : 0u;
   d.nbins = d.W * d.nbc;
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
@@ -314,10 +370,10 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   const MsmDims& d = pl.d;
   const size_t nb = (size_t)d.W * d.B;
   int rc;
-  const uint64_t gen0 = g_alloc_gen;
+  const uint64_t gen0 = g_alloc_gen.load();
 #define ENS(buf, bytes) \
   if ((rc = w.buf.ensure(bytes)) != MSM_OK) return rc
-  ENS(pts, (size_t)d.nm * d.n * PRE_WORDS * 4);
+  ENS(pts, (size_t)(d.shared ? 1 : d.nm) * d.n * PRE_WORDS * 4);
   ENS(err, 16);
   ENS(digits, (size_t)d.W * d.n * 4);
   ENS(hist_rows, (size_t)d.nch * d.nbins * 4);
@@ -344,7 +400,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
 #undef ENS
-  if (g_alloc_gen != gen0) {
+  if (g_alloc_gen.load() != gen0) {
     // err, lead_flag and hist_rows are kept all-zero between MSMs by the kernels themselves
     // (k_bucket_reduce_2 clears the flags, k_part_scatter the histogram rows it consumed), so a
     // replayed graph needs no memset nodes; fresh allocations start that invariant here.
@@ -365,12 +421,21 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
 
 inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Enqueue (parts of) the device pipeline on `s`; the reduced per-window terms land in c->h_out.
-// PART_PRE: memsets, point preparation and the sort; PART_ACC: bucket accumulation;
-// PART_POST: fixup and bucket reduction.
-constexpr int PART_PRE = 1, PART_ACC = 2, PART_POST = 4, PART_ALL = 7;
+// k_prepare_points over `cnt` points of one wire buffer into `pts_out` (one MSM, or one uploaded
+// chunk of it).
+void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint32_t* err, hipStream_t s) {
+  BatchPtrs bp{};
+  bp.p[0] = wire;
+  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(cnt, PP_THREADS), 1), dim3(PP_THREADS), 0, s, bp, pts_out, cnt,
+                     err);
+}
+
+// Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
+// h_out.  `pts` is the point-record buffer (the slot's own, or a shared base vector's).
+// With `acc_events` (eager launches only), k_accumulate runs between the slot's ev_acc0 / ev_acc1;
+// captured graphs get the same events as record nodes (add_acc_event_nodes).
 int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
-                hipStream_t s, int parts = PART_ALL) {
+                hipStream_t s, int parts, uint32_t* pts, bool acc_events = false) {
   const MsmDims& d = pl.d;
   Slot& sl = c->slot[si];
   Workspace& w = sl.ws;
@@ -380,71 +445,79 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   };
   const uint32_t* total = w.bin_base.as<uint32_t>() + d.nbins;
   const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
-  if (parts & PART_PRE) {
-  mark(PH_START);
-  hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.nm), dim3(PP_THREADS), 0, s, d_points, w.pts.as<uint32_t>(), d.n,
-                     w.err.as<uint32_t>());
-  mark(PH_PREPARE);
-  const size_t hist_lds = (size_t)d.Wm * d.nbc * 4;
-  const unsigned rc_grid = grid_for(d.n, RC_SPAN);
-  if (d.c <= 16) {
-    hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                       w.digits.as<uint16_t>(), w.hist_rows.as<uint32_t>());
-  } else {
-    hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                       w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
+  if (parts & PART_PREP) {
+    mark(PH_START);
+    hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, s,
+                       d_points, pts, d.n, w.err.as<uint32_t>());
+    mark(PH_PREPARE);
   }
-  mark(PH_RECODE);
-  hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
-                     w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
-                     d.nbins, w.big_tiles.as<uint32_t>());
-  mark(PH_SCAN);
-  if (d.c <= 16) {
-    hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                       w.digits.as<uint16_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
-                       w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
-  } else {
-    hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                       w.digits.as<uint32_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
-                       w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
+  if (parts & PART_SORT) {
+    if (!(parts & PART_PREP)) {
+      mark(PH_START);
+      mark(PH_PREPARE);
+    }
+    const size_t hist_lds = (size_t)d.Wm * d.nbc * 4;
+    const unsigned rc_grid = grid_for(d.n, RC_SPAN);
+    if (d.c <= 16) {
+      hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+                         w.digits.as<uint16_t>(), w.hist_rows.as<uint32_t>());
+    } else {
+      hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
+                         w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
+    }
+    mark(PH_RECODE);
+    hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
+                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
+                       d.nbins, w.big_tiles.as<uint32_t>());
+    mark(PH_SCAN);
+    if (d.c <= 16) {
+      hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                         w.digits.as<uint16_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
+                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
+    } else {
+      hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                         w.digits.as<uint32_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
+                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
+    }
+    mark(PH_SCATTER);
+    hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
+                       w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
+                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.cursor.as<uint32_t>());
+    hipLaunchKernelGGL(k_big_place, dim3(BP_GRID), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
+                       w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, w.big_tiles.as<uint32_t>(),
+                       w.cursor.as<uint32_t>(), w.sorted_entry.as<uint32_t>());
+    mark(PH_FINE);
   }
-  mark(PH_SCATTER);
-  hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
-                     w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
-                     w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.cursor.as<uint32_t>());
-  hipLaunchKernelGGL(k_big_place, dim3(BP_GRID), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
-                     w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, w.big_tiles.as<uint32_t>(),
-                     w.cursor.as<uint32_t>(), w.sorted_entry.as<uint32_t>());
-  mark(PH_FINE);
-  }
+  if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
   if (parts & PART_ACC) {
-  hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, w.pts.as<uint32_t>(),
-                     w.sorted_entry.as<uint32_t>(), w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total,
-                     pl.K, d.W * d.B, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                     w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
-                     w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
-  mark(PH_ACCUM);
+    hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
+                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
+                       w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                       w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
+                       w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
+    mark(PH_ACCUM);
   }
+  if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
   if (parts & PART_POST) {
-  hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
-                     w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
-                     w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                     w.lead_flag.as<uint32_t>());
-  hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
-                     w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
-  mark(PH_FIXUP);
-  hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : pl.L == 16 ? k_bucket_reduce_1<16> : k_bucket_reduce_1<8>,
-                     dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s, w.buckets.as<uint32_t>(),
-                     w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(),
-                     w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());
-  mark(PH_RED1);
-  hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
-                     w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
-                     w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total,
-                     reinterpret_cast<uint32_t*>(sl.h_out_dev));
-  mark(PH_RED2);
-  mark(PH_READBACK);
+    hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
+                       w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
+                       w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                       w.lead_flag.as<uint32_t>());
+    hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
+                       w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
+    mark(PH_FIXUP);
+    hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : pl.L == 16 ? k_bucket_reduce_1<16> : k_bucket_reduce_1<8>,
+                       dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s,
+                       w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(),
+                       w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());
+    mark(PH_RED1);
+    hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
+                       w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
+                       w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total,
+                       reinterpret_cast<uint32_t*>(sl.h_out_dev));
+    mark(PH_RED2);
+    mark(PH_READBACK);
   }
   HIPCHECK(hipGetLastError());
   return MSM_OK;
@@ -523,25 +596,58 @@ bool graphs_enabled() {
   return on;
 }
 
-void drop_graphs(Slot& sl) {
-  for (int i = 0; i < 3; i++) {
-    if (sl.gexec[i]) hipGraphExecDestroy(sl.gexec[i]);
-    if (sl.graph[i]) hipGraphDestroy(sl.graph[i]);
-    sl.gexec[i] = nullptr;
-    sl.graph[i] = nullptr;
+// Bracket the captured k_accumulate node with event-record nodes (the slot's ev_acc0 / ev_acc1):
+// every replay of the graph then times the accumulation, with no extra launches.
+int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
+  size_t num = 0;
+  if (hipGraphGetNodes(g, nullptr, &num) != hipSuccess || num == 0) return MSM_ERR_HIP;
+  std::vector<hipGraphNode_t> nodes(num);
+  if (hipGraphGetNodes(g, nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
+  const void* f_acc = reinterpret_cast<const void*>(&k_accumulate);
+  hipGraphNode_t acc = nullptr;
+  for (hipGraphNode_t nd : nodes) {
+    hipGraphNodeType ty;
+    hipKernelNodeParams kp{};
+    if (hipGraphNodeGetType(nd, &ty) == hipSuccess && ty == hipGraphNodeTypeKernel &&
+        hipGraphKernelNodeGetParams(nd, &kp) == hipSuccess && kp.func == f_acc)
+      acc = nd;
   }
-  sl.n_prep = sl.n_recode = nullptr;
-  sl.g_pts = sl.g_sc = BatchPtrs{};
+  if (!acc) return MSM_ERR_HIP;
+  size_t nd = 0, nx = 0;
+  if (hipGraphNodeGetDependencies(acc, nullptr, &nd) != hipSuccess ||
+      hipGraphNodeGetDependentNodes(acc, nullptr, &nx) != hipSuccess)
+    return MSM_ERR_HIP;
+  std::vector<hipGraphNode_t> deps(nd), outs(nx);
+  if ((nd && hipGraphNodeGetDependencies(acc, deps.data(), &nd) != hipSuccess) ||
+      (nx && hipGraphNodeGetDependentNodes(acc, outs.data(), &nx) != hipSuccess))
+    return MSM_ERR_HIP;
+  hipGraphNode_t r0 = nullptr, r1 = nullptr;
+  for (hipGraphNode_t d : deps)
+    if (hipGraphRemoveDependencies(g, &d, &acc, 1) != hipSuccess) return MSM_ERR_HIP;
+  if (hipGraphAddEventRecordNode(&r0, g, deps.data(), deps.size(), sl.ev_acc0) != hipSuccess ||
+      hipGraphAddDependencies(g, &r0, &acc, 1) != hipSuccess)
+    return MSM_ERR_HIP;
+  for (hipGraphNode_t o : outs)
+    if (hipGraphRemoveDependencies(g, &acc, &o, 1) != hipSuccess) return MSM_ERR_HIP;
+  if (hipGraphAddEventRecordNode(&r1, g, &acc, 1, sl.ev_acc1) != hipSuccess) return MSM_ERR_HIP;
+  for (hipGraphNode_t o : outs)
+    if (hipGraphAddDependencies(g, &r1, &o, 1) != hipSuccess) return MSM_ERR_HIP;
+  return MSM_OK;
 }
 
 int capture(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, hipStream_t s,
-            int parts, hipGraph_t* gout, hipGraphExec_t* out) {
+            int parts, uint32_t* pts, bool acc_events, hipGraph_t* gout, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return MSM_ERR_HIP;
-  int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts);
+  int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts);
   hipError_t e = hipStreamEndCapture(s, &g);
   if (rc != MSM_OK || e != hipSuccess || !g) {
     if (g) hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return MSM_ERR_HIP;
+  }
+  if (acc_events && (parts & PART_ACC) && add_acc_event_nodes(g, c->slot[si]) != MSM_OK) {
+    hipGraphDestroy(g);
     (void)hipGetLastError();
     return MSM_ERR_HIP;
   }
@@ -556,12 +662,12 @@ int capture(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtr
   return MSM_OK;
 }
 
-// Find the input-reading kernel nodes of slot graph 0 so later launches can repoint them.
-int find_input_nodes(Slot& sl) {
+// Find the input-reading kernel nodes of a segment so later launches can repoint them.
+int find_input_nodes(Segment& sg) {
   size_t num = 0;
-  if (hipGraphGetNodes(sl.graph[0], nullptr, &num) != hipSuccess || num == 0) return MSM_ERR_HIP;
+  if (hipGraphGetNodes(sg.graph, nullptr, &num) != hipSuccess || num == 0) return MSM_ERR_HIP;
   std::vector<hipGraphNode_t> nodes(num);
-  if (hipGraphGetNodes(sl.graph[0], nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
+  if (hipGraphGetNodes(sg.graph, nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
   const void* f_prep = reinterpret_cast<const void*>(&k_prepare_points);
   const void* f_rc16 = reinterpret_cast<const void*>(&k_recode_hist<uint16_t>);
   const void* f_rc32 = reinterpret_cast<const void*>(&k_recode_hist<uint32_t>);
@@ -571,130 +677,158 @@ int find_input_nodes(Slot& sl) {
     hipKernelNodeParams kp{};
     if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess) continue;
     if (kp.func == f_prep) {
-      sl.n_prep = nd;
-      sl.p_prep = kp;
+      sg.n_prep = nd;
+      sg.p_prep = kp;
     } else if (kp.func == f_rc16 || kp.func == f_rc32) {
-      sl.n_recode = nd;
-      sl.p_recode = kp;
+      sg.n_recode = nd;
+      sg.p_recode = kp;
     }
   }
-  return sl.n_prep && sl.n_recode ? MSM_OK : MSM_ERR_HIP;
+  const bool ok = (!(sg.parts & PART_PREP) || sg.n_prep) && (!(sg.parts & PART_SORT) || sg.n_recode);
+  return ok ? MSM_OK : MSM_ERR_HIP;
 }
 
-// Point the instantiated slot graph at new input buffers (kernel-node argument update, no
-// re-capture).
-int repoint_inputs(DevCtx* c, const Plan& pl, Slot& sl, const BatchPtrs& d_points, const BatchPtrs& d_scalars) {
-  const MsmDims& d = pl.d;
-  Workspace& w = sl.ws;
-  BatchPtrs wire = d_points;
-  uint32_t* ptsb = w.pts.as<uint32_t>();
-  uint32_t n = d.n;
-  uint32_t* err = w.err.as<uint32_t>();
-  void* a_prep[] = {&wire, &ptsb, &n, &err};
-  hipKernelNodeParams kp = sl.p_prep;
-  kp.kernelParams = a_prep;
-  kp.extra = nullptr;
-  if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_prep, &kp) != hipSuccess) return MSM_ERR_HIP;
-  BatchPtrs scal = d_scalars;
-  MsmDims dd = d;
-  void* digits = w.digits.p;
-  uint32_t* hist = w.hist_rows.as<uint32_t>();
-  void* a_rc[] = {&scal, &dd, &digits, &hist};
-  hipKernelNodeParams kr = sl.p_recode;
-  kr.kernelParams = a_rc;
-  kr.extra = nullptr;
-  if (hipGraphExecKernelNodeSetParams(sl.gexec[0], sl.n_recode, &kr) != hipSuccess) return MSM_ERR_HIP;
-  sl.g_pts = d_points;
-  sl.g_sc = d_scalars;
-  return MSM_OK;
-}
-
-// Enqueue one MSM in slot `si`.  The launch sequence of each slot is captured into HIP graphs and
-// replayed (one hipGraphLaunch instead of ~14 enqueues); new input buffers only repoint two
-// kernel nodes.  Profiling mode 1 launches eagerly with an event between every phase; mode 2
-// brackets an eager k_accumulate launch with events, between two graphs (pre / post).  Captures
-// only on the library's own stream (a caller's stream may be capturing or in use).
 bool same_ptrs(const BatchPtrs& a, const BatchPtrs& b) { return memcmp(&a, &b, sizeof(BatchPtrs)) == 0; }
 
-int launch_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, hipStream_t s,
-               bool own_stream, bool bracket) {
-  Slot& sl = c->slot[si];
-  const int prof = bracket ? 2 : 0;
-  const bool graphs = own_stream && c->graphs_ok && graphs_enabled() && c->profiling != 1;
-  if (graphs) {
-    Slot::GraphKey key{(size_t)pl.d.n, pl.d.c, pl.K, pl.d.nm, prof, g_alloc_gen};
-    if (!(sl.gexec[0] && key == sl.gkey)) {
-      drop_graphs(sl);
-      int rc;
-      if (prof == 2) {
-        rc = capture(c, pl, d_points, d_scalars, si, s, PART_PRE, &sl.graph[0], &sl.gexec[0]);
-        if (rc == MSM_OK) rc = capture(c, pl, d_points, d_scalars, si, s, PART_POST, &sl.graph[2], &sl.gexec[2]);
-      } else {
-        rc = capture(c, pl, d_points, d_scalars, si, s, PART_ALL, &sl.graph[0], &sl.gexec[0]);
-      }
-      if (rc == MSM_OK) rc = find_input_nodes(sl);
-      if (rc != MSM_OK) {
-        drop_graphs(sl);
-        c->graphs_ok = false;  // capture unsupported here: stay eager
-      } else {
-        sl.gkey = key;
-        sl.g_pts = d_points;
-        sl.g_sc = d_scalars;
-      }
-    }
-    if (c->graphs_ok && (!same_ptrs(sl.g_pts, d_points) || !same_ptrs(sl.g_sc, d_scalars)) &&
-        repoint_inputs(c, pl, sl, d_points, d_scalars) != MSM_OK) {
-      drop_graphs(sl);
-      (void)hipGetLastError();
-      c->graphs_ok = false;
-    }
+// Point an instantiated segment at new input buffers (kernel-node argument update, no
+// re-capture).
+int repoint_inputs(const Plan& pl, Slot& sl, Segment& sg, const BatchPtrs& d_points, const BatchPtrs& d_scalars) {
+  const MsmDims& d = pl.d;
+  Workspace& w = sl.ws;
+  if (sg.n_prep && !same_ptrs(sg.in_pts, d_points)) {
+    BatchPtrs wire = d_points;
+    uint32_t* ptsb = const_cast<uint32_t*>(sg.pts_buf);
+    uint32_t n = d.n;
+    uint32_t* err = w.err.as<uint32_t>();
+    void* a_prep[] = {&wire, &ptsb, &n, &err};
+    hipKernelNodeParams kp = sg.p_prep;
+    kp.kernelParams = a_prep;
+    kp.extra = nullptr;
+    if (hipGraphExecKernelNodeSetParams(sg.exec, sg.n_prep, &kp) != hipSuccess) return MSM_ERR_HIP;
+    sg.in_pts = d_points;
   }
-  const bool use_graphs = graphs && c->graphs_ok;
-  if (prof == 2) {
-    HIPCHECK(hipEventRecord(sl.ev_start, s));
-    if (use_graphs) {
-      HIPCHECK(hipGraphLaunch(sl.gexec[0], s));
-    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_PRE)) {
-      return rc;
-    }
-    // k_accumulate itself is launched eagerly between its two events: a graph launch there would
-    // put the graph's own launch latency inside the measured bracket
-    HIPCHECK(hipEventRecord(sl.ev_acc0, s));
-    if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC)) return rc;
-    HIPCHECK(hipEventRecord(sl.ev_acc1, s));
-    if (use_graphs) {
-      HIPCHECK(hipGraphLaunch(sl.gexec[2], s));
-    } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_POST)) {
-      return rc;
-    }
-    HIPCHECK(hipEventRecord(sl.ev_end, s));
-    return MSM_OK;
+  if (sg.n_recode && !same_ptrs(sg.in_sc, d_scalars)) {
+    BatchPtrs scal = d_scalars;
+    MsmDims dd = d;
+    void* digits = w.digits.p;
+    uint32_t* hist = w.hist_rows.as<uint32_t>();
+    void* a_rc[] = {&scal, &dd, &digits, &hist};
+    hipKernelNodeParams kr = sg.p_recode;
+    kr.kernelParams = a_rc;
+    kr.extra = nullptr;
+    if (hipGraphExecKernelNodeSetParams(sg.exec, sg.n_recode, &kr) != hipSuccess) return MSM_ERR_HIP;
+    sg.in_sc = d_scalars;
   }
-  if (use_graphs) {
-    HIPCHECK(hipGraphLaunch(sl.gexec[0], s));
-    return MSM_OK;
-  }
-  return enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ALL);
-}
-
-// Start one MSM (device-resident inputs) in slot `si`; returns once it is enqueued.
-int submit_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
-               hipStream_t s) {
-  Slot& sl = c->slot[si];
-  sl.pl = pl;
-  // profiling mode 2 brackets k_accumulate with events on every PROF_EVERY-th MSM only (each
-  // bracket costs ~20 us of launch gaps); the mean over those is the reported duration
-  sl.bracketed = c->profiling == 2 && (c->prof_seq++ % PROF_EVERY) == 0;
-  int rc = launch_msm(c, pl, d_points, d_scalars, si, s, s == sl.stream, sl.bracketed);
-  if (rc != MSM_OK) return rc;
-  HIPCHECK(hipEventRecord(sl.ev_done, s));
   return MSM_OK;
 }
 
-// Wait for the MSM in slot `si` (spinning briefly: the result is usually due within a couple of
+// The cached graph of `parts` for this plan (captured on first use, least recently used segment
+// evicted), repointed at the launch's inputs; nullptr when graphs are unavailable.
+Segment* get_segment(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
+                     int parts, uint32_t* pts, bool acc_events) {
+  Slot& sl = c->slot[si];
+  const uint64_t gen = g_alloc_gen.load();
+  Segment* hit = nullptr;
+  for (Segment& sg : sl.seg)
+    if (sg.exec && sg.parts == parts && sg.pts_buf == pts && sg.acc_events == acc_events && sg.gen == gen &&
+        plan_eq(sg.pl, pl))
+      hit = &sg;
+  if (!hit) {
+    Segment* victim = &sl.seg[0];
+    for (Segment& sg : sl.seg) {
+      if (!sg.exec || sg.gen != gen) {
+        victim = &sg;
+        break;
+      }
+      if (sg.used < victim->used) victim = &sg;
+    }
+    victim->drop();
+    victim->pl = pl;
+    victim->parts = parts;
+    victim->pts_buf = pts;
+    victim->acc_events = acc_events;
+    victim->gen = gen;
+    int rc = capture(c, pl, d_points, d_scalars, si, sl.stream, parts, pts, acc_events, &victim->graph,
+                     &victim->exec);
+    if (rc == MSM_OK) rc = find_input_nodes(*victim);
+    if (rc != MSM_OK) {
+      victim->drop();
+      // event-record nodes unsupported: time k_accumulate eagerly between graph segments;
+      // otherwise capture itself is unsupported here: stay eager
+      if (acc_events) c->graph_events_ok = false;
+      else c->graphs_ok = false;
+      return nullptr;
+    }
+    victim->in_pts = d_points;
+    victim->in_sc = d_scalars;
+    hit = victim;
+  }
+  if (repoint_inputs(pl, sl, *hit, d_points, d_scalars) != MSM_OK) {
+    hit->drop();
+    (void)hipGetLastError();
+    c->graphs_ok = false;
+    return nullptr;
+  }
+  hit->used = ++sl.seg_clock;
+  return hit;
+}
+
+// Enqueue `parts` of one launch in slot `si` (on the slot's stream) by replaying the captured
+// graph of those parts; k_accumulate runs between the slot's two timing events on every launch
+// (event-record nodes inside the graph), so the production path is the timed one.  Where the
+// runtime cannot capture event records, the accumulation is launched eagerly between a graph of
+// the parts before it and one of the parts after it.  Profiling mode 1 launches everything
+// eagerly with an event between every phase.
+int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
+                 int parts, uint32_t* pts) {
+  Slot& sl = c->slot[si];
+  hipStream_t s = sl.stream;
+  const bool acc = (parts & PART_ACC) != 0;
+  sl.acc_timed = acc;
+  if (parts & (PART_PREP | PART_SORT)) HIPCHECK(hipEventRecord(sl.ev_start, s));
+  if (c->profiling == 1) {
+    sl.acc_timed = false;
+    if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts)) return rc;
+  } else if (c->graphs_ok && graphs_enabled()) {
+    Segment* sg = c->graph_events_ok ? get_segment(c, pl, d_points, d_scalars, si, parts, pts, acc) : nullptr;
+    if (sg) {
+      HIPCHECK(hipGraphLaunch(sg->exec, s));
+    } else {
+      auto run = [&](int p) -> int {
+        if (!p) return MSM_OK;
+        Segment* g = c->graphs_ok ? get_segment(c, pl, d_points, d_scalars, si, p, pts, false) : nullptr;
+        if (g) {
+          HIPCHECK(hipGraphLaunch(g->exec, s));
+          return MSM_OK;
+        }
+        return enqueue_msm(c, pl, d_points, d_scalars, si, s, p, pts);
+      };
+      if (int rc = run(parts & (PART_PREP | PART_SORT))) return rc;
+      if (acc)
+        if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC, pts, true)) return rc;
+      if (int rc = run(parts & PART_POST)) return rc;
+    }
+  } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts, acc)) {
+    return rc;
+  }
+  if (parts & PART_POST) {
+    HIPCHECK(hipEventRecord(sl.ev_end, s));
+    HIPCHECK(hipEventRecord(sl.ev_done, s));
+  }
+  return MSM_OK;
+}
+
+// Make the slot's stream wait for its inputs: uploads on the copy stream and/or the caller's
+// stream (recorded into ev_in / ev_user beforehand).
+int wait_event(hipStream_t s, hipEvent_t e) {
+  HIPCHECK(hipStreamWaitEvent(s, e, 0));
+  return MSM_OK;
+}
+
+// Wait for the launch in slot `si` (spinning briefly: the result is usually due within a couple of
 // milliseconds, and a blocking wait adds a wake-up latency) and take its window terms.  With
-// `terms` the terms are copied out, so the slot can take its next MSM before the host tail runs
-// (finish_terms); otherwise the host tail runs here, on the pinned buffer.
+// `terms` the terms are copied out, so the slot can take its next launch before the host tail
+// runs; otherwise the host tail runs here, on the pinned buffer.
 int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr) {
   Slot& sl = c->slot[si];
   const Plan& pl = sl.pl;
@@ -715,7 +849,7 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
   else
     *result = horner_tail(pl, h);
   auto t1 = clk::now();
-  if (c->profiling == 1 || (c->profiling == 2 && sl.bracketed)) {
+  if (c->profiling == 1 || (c->profiling == 2 && sl.acc_timed)) {
     float ms[PH_COUNT] = {};
     msm_profile_t& P = c->last;
     if (c->profiling == 1) {
@@ -741,10 +875,57 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
     P.windows = pl.d.Wm;
     P.run_length = pl.K;
     P.chunk_len = pl.L;
+    P.msms_per_launch = pl.d.nm;
     P.accumulate_sum += P.accumulate;
     P.device_total_sum += P.device_total;
     P.profiled++;
+    if (c->profiling == 2) {
+      float a = 0, b = 0;
+      if (hipEventElapsedTime(&a, c->ev_base, sl.ev_acc0) == hipSuccess &&
+          hipEventElapsedTime(&b, c->ev_base, sl.ev_acc1) == hipSuccess)
+        c->acc_ivals.emplace_back(a, b);
+    }
   }
+  return MSM_OK;
+}
+
+// Profiling mode 2: the call's accumulation intervals start from ev_base; at the end their union
+// (wall time with at least one k_accumulate in flight) is added to accumulate_union_sum.  With
+// several launches in flight accumulations may overlap each other, so the union, not the sum of
+// brackets, is the kernel's share of the device time.
+void begin_call(DevCtx* c) {
+  c->acc_ivals.clear();
+  if (c->profiling == 2) hipEventRecord(c->ev_base, c->slot[0].stream);
+}
+void end_call(DevCtx* c) {
+  if (c->profiling != 2 || c->acc_ivals.empty()) return;
+  std::sort(c->acc_ivals.begin(), c->acc_ivals.end());
+  double total = 0, lo = c->acc_ivals[0].first, hi = c->acc_ivals[0].second;
+  for (const auto& iv : c->acc_ivals) {
+    if (iv.first > hi) {
+      total += hi - lo;
+      lo = iv.first;
+      hi = iv.second;
+    } else {
+      hi = std::max<double>(hi, iv.second);
+    }
+  }
+  total += hi - lo;
+  c->last.accumulate_union_sum += total;
+  c->acc_ivals.clear();
+}
+
+BatchPtrs splat(const uint32_t* p) {
+  BatchPtrs b{};
+  for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) b.p[m] = p;
+  return b;
+}
+
+// The caller's stream (if any) -> every slot stream about to be used waits for its work so far.
+int order_after_user(DevCtx* c, hipStream_t user, int nslot) {
+  if (!user) return MSM_OK;
+  HIPCHECK(hipEventRecord(c->ev_user, user == (hipStream_t)MSM_STREAM_NULL ? nullptr : user));
+  for (int si = 0; si < nslot; si++) HIPCHECK(hipStreamWaitEvent(c->slot[si].stream, c->ev_user, 0));
   return MSM_OK;
 }
 
@@ -760,20 +941,114 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if (rc != MSM_OK) return rc;
   const int si = 0;  // a lone MSM always uses slot 0 (the other workspaces only for pipelining)
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
-  hipStream_t s = user_stream ? user_stream : c->slot[si].stream;
-  BatchPtrs bp{}, bs{};
-  for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
-    bp.p[m] = d_points;
-    bs.p[m] = d_scalars;
+  if ((rc = order_after_user(c, user_stream, 1)) != MSM_OK) return rc;
+  c->slot[si].pl = pl;
+  if ((rc = launch_parts(c, pl, splat(d_points), splat(d_scalars), si, PART_ALL, c->slot[si].ws.pts.as<uint32_t>())))
+    return rc;
+  return finish_msm(c, si, result);
+}
+
+// Host -> device copy of one input array on the copy stream, in pieces of `piece` bytes; after
+// each piece `on_piece(off, bytes)` may hand the uploaded range to the device (an event on the
+// copy stream marks it).  hipMemcpyAsync stages pageable memory itself at the PCIe rate
+// (tools/ubench/h2d_bench.cpp: 56 GB/s pageable or pinned), so no extra host copy is made.
+template <typename F>
+int upload(DevCtx* c, void* dst, const void* src, size_t bytes, size_t piece, F&& on_piece) {
+  for (size_t off = 0; off < bytes; off += piece) {
+    const size_t b = std::min(piece, bytes - off);
+    HIPCHECK(hipMemcpyAsync(static_cast<char*>(dst) + off, static_cast<const char*>(src) + off, b,
+                            hipMemcpyHostToDevice, c->copy_stream));
+    if (int rc = on_piece(off, b)) return rc;
   }
-  if ((rc = submit_msm(c, pl, bp, bs, si, s)) != MSM_OK) return rc;
+  return MSM_OK;
+}
+
+constexpr size_t UPLOAD_PTS_PIECE = 65536;  // points per uploaded piece (8 MiB; a multiple of PP_THREADS)
+
+// Upload n host points into `wire` and prepare them into `pts` piece by piece on stream `s`: the
+// preparation of piece k overlaps the upload of piece k+1 (the reference's staging ring,
+// gpu.ts:146-155, without its 128 MiB cap).
+int upload_points(DevCtx* c, const uint32_t* points_be, size_t n, uint32_t* wire, uint32_t* pts, uint32_t* err,
+                  hipStream_t s) {
+  int k = 0;
+  return upload(c, wire, points_be, n * 128, UPLOAD_PTS_PIECE * 128, [&](size_t off, size_t b) -> int {
+    hipEvent_t e = c->ev_chunk[k++ % NCHUNK_EV];
+    HIPCHECK(hipEventRecord(e, c->copy_stream));
+    HIPCHECK(hipStreamWaitEvent(s, e, 0));
+    const size_t p0 = off / 128;
+    launch_prepare(wire + p0 * 32, pts + p0 * PRE_WORDS, (uint32_t)(b / 128), err, s);
+    HIPCHECK(hipGetLastError());
+    return MSM_OK;
+  });
+}
+
+// Upload a scalar vector into `wire` and make stream `s` wait for it.
+int upload_scalars(DevCtx* c, const uint32_t* scalars_be, size_t n, uint32_t* wire, hipStream_t s, hipEvent_t e) {
+  int rc = upload(c, wire, scalars_be, n * 32, n * 32, [](size_t, size_t) { return MSM_OK; });
+  if (rc != MSM_OK) return rc;
+  HIPCHECK(hipEventRecord(e, c->copy_stream));
+  HIPCHECK(hipStreamWaitEvent(s, e, 0));
+  return MSM_OK;
+}
+
+// The caller's host array, pinned in place for the call when MSM_H2D_PIN=1 (hipHostRegister:
+// the pieces' copies then DMA straight from it, asynchronously).  Pinned memory is used as is.
+struct HostPin {
+  DevCtx* c = nullptr;
+  void* p = nullptr;
+  bool reg = false;
+  HostPin(DevCtx* ctx, const void* ptr, size_t bytes) : c(ctx) {
+    static const bool on = getenv("MSM_H2D_PIN") && atoi(getenv("MSM_H2D_PIN")) == 1;
+    if (!on || !bytes) return;
+    if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess) {
+      p = const_cast<void*>(ptr);
+      reg = true;
+    } else {
+      (void)hipGetLastError();  // already pinned, or not registrable: plain copies
+    }
+  }
+  ~HostPin() {
+    if (!reg) return;
+    hipStreamSynchronize(c->copy_stream);  // no copy may still read it
+    hipHostUnregister(p);
+  }
+};
+
+// One MSM of host-resident inputs: the scalars go up first and the bucket sort starts on them
+// while the points upload piece by piece, each piece prepared as it lands; accumulation starts
+// after the last piece.  The end-to-end time is then ~ PCIe transfer + the post-upload tail.
+int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
+             Pt* result) {
+  if (n == 0) {
+    *result = pt_identity();
+    return MSM_OK;
+  }
+  Plan pl;
+  int rc = make_plan(n, o, c->n_cu, &pl);
+  if (rc != MSM_OK) return rc;
+  const int si = 0;
+  Slot& sl = c->slot[si];
+  Workspace& w = sl.ws;
+  if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
+  if ((rc = w.wire_pts.ensure(n * 128)) != MSM_OK || (rc = w.wire_sc.ensure(n * 32)) != MSM_OK) return rc;
+  sl.pl = pl;
+  uint32_t* pts = w.pts.as<uint32_t>();
+  const BatchPtrs bp = splat(w.wire_pts.as<uint32_t>()), bs = splat(w.wire_sc.as<uint32_t>());
+  HostPin pin_sc(c, scalars_be, n * 32), pin_pts(c, points_be, n * 128);
+  if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK) return rc;
+  if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return rc;
+  if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
+    return rc;
+  if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return rc;
   return finish_msm(c, si, result);
 }
 
 // MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
 // and sort kernels leave most of the chip idle), so several run side by side; MSM_SLOTS
-// overrides (1 = everything in order on one stream: clean per-kernel profiles).
-int pipeline_slots(size_t n) {
+// overrides (1 = everything in order on one stream: clean per-kernel profiles), and so does the
+// MSM_FLAG_SERIAL option flag.
+int pipeline_slots(size_t n, const msm_opts* o) {
+  if (o && (o->flags & MSM_FLAG_SERIAL)) return 1;
   static const int env = getenv("MSM_SLOTS") ? atoi(getenv("MSM_SLOTS")) : 0;
   if (env >= 1) return std::min(env, NSLOT);
   (void)n;
@@ -791,16 +1066,25 @@ uint32_t pipeline_batch(size_t n, size_t count) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
-// `count` MSMs of n points each, pipelined over pipeline_slots(n) slots, each with its own stream
-// and workspace, in launches of pipeline_batch MSMs (the last batch is padded by repeating its
-// last MSM, whose extra results are dropped): later batches are enqueued before the host
-// finishes batch j, so the host tail (window Horner) of one overlaps the device work of the
-// next, and the batches' kernels may overlap on the device (the latency-bound reduction of one
-// beside another's sort and accumulation).  With a caller-supplied stream everything runs in
-// order on it.  Results go out affine (16 words each) or, with `projective`, as X|Y|T|Z
-// partials (32 words).
-int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* d_scalars, size_t n, size_t count,
-             const msm_opts* o, hipStream_t user_stream, uint32_t* out_be, bool projective) {
+// Where the inputs of one pipelined run come from.
+struct ManyInputs {
+  enum Kind { DEVICE, HOST } kind = DEVICE;
+  const uint32_t* const* points = nullptr;  // per MSM (ignored when shared_points is set)
+  const uint32_t* const* scalars = nullptr;
+  const uint32_t* shared_points = nullptr;  // one base vector for every MSM (prover batch)
+};
+
+// `count` MSMs of n points each, pipelined over pipeline_slots slots, each with its own stream and
+// workspace, in launches of pipeline_batch MSMs (the last launch is padded by repeating its last
+// MSM, whose extra results are dropped): later launches are enqueued before the host finishes
+// launch j, so the host tail (window Horner) of one overlaps the device work of the next, and
+// the launches' kernels overlap on the device (the latency-bound reduction of one beside
+// another's sort and accumulation).  Host inputs are uploaded on the copy stream into the
+// slot's wire buffers, overlapping the other slots' kernels.  A shared base vector is prepared
+// once, before the first launch, and every launch reads its records.  Results go out affine (16
+// words each) or, with `projective`, as X|Y|T|Z partials (32 words).
+int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_opts* o, hipStream_t user_stream,
+             uint32_t* out_be, bool projective) {
   auto emit = [&](const Pt& r, size_t b) {
     if (projective)
       pt_to_be_xyzt(r, out_be + 32 * b);
@@ -811,39 +1095,94 @@ int run_many(DevCtx* c, const uint32_t* const* d_points, const uint32_t* const* 
     for (size_t b = 0; b < count; b++) emit(pt_identity(), b);
     return MSM_OK;
   }
+  const bool shared = in.shared_points != nullptr;
+  const bool host = in.kind == ManyInputs::HOST;
   for (size_t b = 0; b < count; b++)
-    if (!d_points[b] || !d_scalars[b]) return MSM_ERR_INVALID_ARG;
+    if ((!shared && !in.points[b]) || !in.scalars[b]) return MSM_ERR_INVALID_ARG;
   const uint32_t nm = pipeline_batch(n, count);
   const size_t nbatch = (count + nm - 1) / nm;
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm);
+  int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm, shared);
   if (rc != MSM_OK) return rc;
-  const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)pipeline_slots(n)) : 1;
-  for (int si = 0; si < nslot; si++)
+  const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)pipeline_slots(n, o)) : 1;
+  for (int si = 0; si < nslot; si++) {
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
-  auto stream_of = [&](int si) { return user_stream ? user_stream : c->slot[si].stream; };
-  // Batch j goes to slot j % nslot.  Its previous occupant, batch j - nslot, is waited for and
-  // its window terms copied out just before; the host tail (window Horner) of batch j - nslot
-  // runs after j is enqueued, so the device holds nslot batches while the host works
-  // (otherwise batches that finish together leave the device idle for a Horner each).
-  std::vector<uint32_t> terms;
+    if (host) {
+      Workspace& w = c->slot[si].ws;
+      if ((!shared && (rc = w.wire_pts.ensure((size_t)nm * n * 128)) != MSM_OK) ||
+          (rc = w.wire_sc.ensure((size_t)nm * n * 32)) != MSM_OK)
+        return rc;
+    }
+  }
+  if ((rc = order_after_user(c, user_stream, nslot)) != MSM_OK) return rc;
   auto fail = [&](int code) {
-    for (int k = 0; k < nslot; k++) hipStreamSynchronize(stream_of(k));
+    hipStreamSynchronize(c->copy_stream);
+    for (int k = 0; k < nslot; k++) hipStreamSynchronize(c->slot[k].stream);
     return code;
   };
+  uint32_t* pts_shared = nullptr;
+  if (shared) {
+    // the base vector's records, prepared once on slot 0's stream; the other slots wait for them
+    if ((rc = c->shared_pts.ensure(n * PRE_WORDS * 4)) != MSM_OK) return rc;
+    pts_shared = c->shared_pts.as<uint32_t>();
+    Slot& s0 = c->slot[0];
+    if (host) {
+      if ((rc = s0.ws.wire_pts.ensure(n * 128)) != MSM_OK) return rc;
+      rc = upload_points(c, in.shared_points, n, s0.ws.wire_pts.as<uint32_t>(), pts_shared, s0.ws.err.as<uint32_t>(),
+                         s0.stream);
+      if (rc != MSM_OK) return fail(rc);
+    } else {
+      launch_prepare(in.shared_points, pts_shared, (uint32_t)n, s0.ws.err.as<uint32_t>(), s0.stream);
+      if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
+    }
+    if (hipEventRecord(c->ev_shared, s0.stream) != hipSuccess) return fail(MSM_ERR_HIP);
+    for (int si = 1; si < nslot; si++)
+      if (hipStreamWaitEvent(c->slot[si].stream, c->ev_shared, 0) != hipSuccess) return fail(MSM_ERR_HIP);
+  }
+  // Launch j goes to slot j % nslot.  Its previous occupant, launch j - nslot, is waited for and
+  // its window terms copied out just before; the host tail (window Horner) of launch j - nslot
+  // runs after j is enqueued, so the device holds nslot launches while the host works
+  // (otherwise launches that finish together leave the device idle for a Horner each).
+  std::vector<uint32_t> terms;
   for (size_t j = 0; j < nbatch + nslot; j++) {
     const bool have = j >= (size_t)nslot;
     const size_t f = have ? j - nslot : 0;
     if (have && (rc = finish_msm(c, (int)(f % nslot), nullptr, &terms)) != MSM_OK) return fail(rc);
     if (j < nbatch) {
+      const int si = (int)(j % nslot);
+      Slot& sl = c->slot[si];
       BatchPtrs bp{}, bs{};
       for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
         const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
-        bp.p[m] = d_points[b];
-        bs.p[m] = d_scalars[b];
+        bp.p[m] = shared ? in.shared_points : in.points[b];
+        bs.p[m] = in.scalars[b];
+        if (host && m < nm) {
+          // this slot's previous launch has finished (above): its wire buffers are free
+          uint32_t* wsc = sl.ws.wire_sc.as<uint32_t>() + (size_t)m * n * 8;
+          if (hipMemcpyAsync(wsc, in.scalars[b], n * 32, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+            return fail(MSM_ERR_HIP);
+          bs.p[m] = wsc;
+          if (!shared) {
+            uint32_t* wp = sl.ws.wire_pts.as<uint32_t>() + (size_t)m * n * 32;
+            if (hipMemcpyAsync(wp, in.points[b], n * 128, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+              return fail(MSM_ERR_HIP);
+            bp.p[m] = wp;
+          }
+        }
       }
-      const int si = (int)(j % nslot);
-      if ((rc = submit_msm(c, pl, bp, bs, si, stream_of(si))) != MSM_OK) return fail(rc);
+      if (host) {
+        for (uint32_t m = nm; m < MSM_MAX_BATCH; m++) {
+          bp.p[m] = bp.p[nm - 1];
+          bs.p[m] = bs.p[nm - 1];
+        }
+        if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
+            hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
+          return fail(MSM_ERR_HIP);
+      }
+      sl.pl = pl;
+      const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
+      if ((rc = launch_parts(c, pl, bp, bs, si, parts, shared ? pts_shared : sl.ws.pts.as<uint32_t>())) != MSM_OK)
+        return fail(rc);
     }
     if (have)
       for (uint32_t m = 0; m < nm && f * nm + m < count; m++) emit(horner_tail(pl, terms.data(), m), f * nm + m);
@@ -869,21 +1208,41 @@ struct DeviceGuard {
   }
 };
 
-int run_host(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts, Pt* result) {
+// Lock the device context of `opts` and run `fn(ctx)` with its device current.
+template <typename F>
+int on_device(const msm_opts* opts, F&& fn) {
   DevCtx* c;
   int rc = with_device(opts, &c);
   if (rc != MSM_OK) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  if (n == 0) {
-    *result = pt_identity();
-    return MSM_OK;
-  }
-  if ((rc = c->wire_points.ensure(n * 128)) != MSM_OK) return rc;
-  if ((rc = c->wire_scalars.ensure(n * 32)) != MSM_OK) return rc;
-  HIPCHECK(hipMemcpyAsync(c->wire_points.p, points_be, n * 128, hipMemcpyHostToDevice, c->slot[0].stream));
-  HIPCHECK(hipMemcpyAsync(c->wire_scalars.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->slot[0].stream));
-  return run_device(c, c->wire_points.as<uint32_t>(), c->wire_scalars.as<uint32_t>(), n, opts, nullptr, result);
+  c->profiling = g_profiling;
+  begin_call(c);
+  rc = fn(c);
+  end_call(c);
+  return rc;
+}
+
+int host_entry(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts, Pt* r) {
+  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  return on_device(opts, [&](DevCtx* c) { return run_host(c, points_be, scalars_be, n, opts, r); });
+}
+
+int device_entry(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                 void* hip_stream, Pt* r) {
+  if ((!d_points_be || !d_scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  return on_device(opts, [&](DevCtx* c) {
+    return run_device(c, d_points_be, d_scalars_be, n, opts, (hipStream_t)hip_stream, r);
+  });
+}
+
+int many_entry(const ManyInputs& in, size_t n, size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out,
+               bool projective) {
+  if (!out || (!in.scalars && count) || (!in.points && !in.shared_points && count)) return MSM_ERR_INVALID_ARG;
+  if (count == 0) return MSM_OK;
+  return on_device(opts, [&](DevCtx* c) {
+    return run_many(c, in, n, count, opts, (hipStream_t)hip_stream, out, projective);
+  });
 }
 
 }  // namespace
@@ -903,19 +1262,24 @@ void msm_shutdown(void) {
     int prev = 0;
     hipGetDevice(&prev);
     hipSetDevice(c->device);
+    hipStreamSynchronize(c->copy_stream);
     for (Slot& sl : c->slot) hipStreamSynchronize(sl.stream);
-    c->wire_points.release();
-    c->wire_scalars.release();
+    c->shared_pts.release();
     for (Slot& sl : c->slot) {
       sl.ws.release();
-      drop_graphs(sl);
+      for (Segment& sg : sl.seg) sg.drop();
       sl.h_out.release();
       sl.h_out_dev = nullptr;
-      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done})
+      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in})
         if (e) hipEventDestroy(e);
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < NCHUNK_EV; i++) hipEventDestroy(c->ev_chunk[i]);
+    hipEventDestroy(c->ev_user);
+    hipEventDestroy(c->ev_shared);
+    hipEventDestroy(c->ev_base);
     for (Slot& sl : c->slot) hipStreamDestroy(sl.stream);
+    hipStreamDestroy(c->copy_stream);
     hipSetDevice(prev);
   }
   for (DevCtx*& c : g_ctx) {
@@ -956,10 +1320,9 @@ uint32_t msm_best_window(size_t n) {
 
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                 uint32_t out_xy_be[16]) {
-  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
   if (!out_xy_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = run_host(points_be, scalars_be, n, opts, &r);
+  int rc = host_entry(points_be, scalars_be, n, opts, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
@@ -967,24 +1330,12 @@ int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n,
 
 int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                         uint32_t out_xyzt_be[32]) {
-  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
   if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = run_host(points_be, scalars_be, n, opts, &r);
+  int rc = host_entry(points_be, scalars_be, n, opts, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_xyzt(r, out_xyzt_be);
   return MSM_OK;
-}
-
-static int device_entry(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
-                        void* hip_stream, Pt* r) {
-  if ((!d_points_be || !d_scalars_be) && n) return MSM_ERR_INVALID_ARG;
-  DevCtx* c;
-  int rc = with_device(opts, &c);
-  if (rc != MSM_OK) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  return run_device(c, d_points_be, d_scalars_be, n, opts, (hipStream_t)hip_stream, r);
 }
 
 int msm_compute_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
@@ -1009,27 +1360,19 @@ int msm_compute_device_partial(const uint32_t* d_points_be, const uint32_t* d_sc
 
 int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
                             size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be) {
-  if (!out_xy_be || ((!d_points_be || !d_scalars_be) && count)) return MSM_ERR_INVALID_ARG;
-  if (count == 0) return MSM_OK;
-  DevCtx* c;
-  int rc = with_device(opts, &c);
-  if (rc != MSM_OK) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xy_be, false);
+  ManyInputs in;
+  in.points = d_points_be;
+  in.scalars = d_scalars_be;
+  return many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
 }
 
 int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be,
                                     size_t n, size_t count, const msm_opts* opts, void* hip_stream,
                                     uint32_t* out_xyzt_be) {
-  if (!out_xyzt_be || ((!d_points_be || !d_scalars_be) && count)) return MSM_ERR_INVALID_ARG;
-  if (count == 0) return MSM_OK;
-  DevCtx* c;
-  int rc = with_device(opts, &c);
-  if (rc != MSM_OK) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  return run_many(c, d_points_be, d_scalars_be, n, count, opts, (hipStream_t)hip_stream, out_xyzt_be, true);
+  ManyInputs in;
+  in.points = d_points_be;
+  in.scalars = d_scalars_be;
+  return many_entry(in, n, count, opts, hip_stream, out_xyzt_be, true);
 }
 
 int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
@@ -1041,6 +1384,36 @@ int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scal
     ss[b] = d_scalars_be + b * n * 8;
   }
   return msm_compute_many_device(pp.data(), ss.data(), n, count, opts, hip_stream, out_xy_be);
+}
+
+int msm_compute_shared_device(const uint32_t* d_points_be, const uint32_t* const* d_scalars_be, size_t n,
+                              size_t count, const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be) {
+  if (!d_points_be && n && count) return MSM_ERR_INVALID_ARG;
+  ManyInputs in;
+  in.shared_points = d_points_be;
+  in.scalars = d_scalars_be;
+  if (!n) in.points = d_scalars_be;  // n = 0: identities, no input is read
+  return many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
+}
+
+int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
+                     const msm_opts* opts, uint32_t* out_xy_be) {
+  ManyInputs in;
+  in.kind = ManyInputs::HOST;
+  in.points = points_be;
+  in.scalars = scalars_be;
+  return many_entry(in, n, count, opts, nullptr, out_xy_be, false);
+}
+
+int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
+                       const msm_opts* opts, uint32_t* out_xy_be) {
+  if (!points_be && n && count) return MSM_ERR_INVALID_ARG;
+  ManyInputs in;
+  in.kind = ManyInputs::HOST;
+  in.shared_points = points_be;
+  in.scalars = scalars_be;
+  if (!n) in.points = scalars_be;
+  return many_entry(in, n, count, opts, nullptr, out_xy_be, false);
 }
 
 int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]) {
@@ -1096,15 +1469,21 @@ int msm_split(uint32_t c, const uint32_t* scalars_be, size_t n, uint32_t* out) {
   return MSM_OK;
 }
 
+int msm_compute_cpu(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, uint32_t window_bits,
+                    int n_threads, uint32_t out_xy_be[16]) {
+  if (!out_xy_be || ((!points_be || !scalars_be) && n)) return MSM_ERR_INVALID_ARG;
+  return cpu_msm(points_be, scalars_be, n, window_bits, n_threads, out_xy_be);
+}
+
 int msm_set_profiling(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_profiling = enable < 0 ? 0 : enable > 2 ? 1 : enable;
   for (DevCtx* c : g_ctx)
     if (c) {
+      std::lock_guard<std::mutex> lk2(c->mu);  // a call in flight on another thread finishes first
       c->profiling = g_profiling;
-      c->last.accumulate_sum = c->last.device_total_sum = 0;
+      c->last.accumulate_sum = c->last.device_total_sum = c->last.accumulate_union_sum = 0;
       c->last.profiled = 0;
-      c->prof_seq = 0;
     }
   return MSM_OK;
 }

@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
   uint32_t* lstart = dyn + d.nbc;
   uint32_t* gstart = dyn + 2 * d.nbc;
   const uint32_t w = blockIdx.y, ck = blockIdx.x;
-  const uint32_t pbase = (w / d.Wm) * d.n;  // first point record of this window's MSM
+  const uint32_t pbase = d.shared ? 0u : (w / d.Wm) * d.n;  // first point record of this window's MSM
   const size_t row = ((size_t)w * d.nch + ck) * d.nbc;
   for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
     lcur[b] = hist_rows[row + b];

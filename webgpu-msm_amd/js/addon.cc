@@ -32,7 +32,12 @@ namespace {
 struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
-  std::vector<uint32_t> points, scalars;
+  std::vector<uint32_t> points, scalars;  // marshalled BigInt inputs (computeMsmBigInt)
+  // computeMsmU32: the caller's typed arrays, held by references until the job completes and read
+  // in place by msm_compute (no staging copy; they must not be written while the promise is pending)
+  napi_ref ref_points = nullptr, ref_scalars = nullptr;
+  const uint32_t* p_points = nullptr;
+  const uint32_t* p_scalars = nullptr;
   size_t n = 0;
   uint32_t window = 0;
   uint32_t out[16] = {0};
@@ -45,7 +50,9 @@ void execute(napi_env, void* data) {
   memset(&o, 0, sizeof(o));
   o.window_bits = j->window;
   o.device = -1;
-  j->rc = msm_compute(j->points.data(), j->scalars.data(), j->n, &o, j->out);
+  const uint32_t* pts = j->p_points ? j->p_points : j->points.data();
+  const uint32_t* sc = j->p_scalars ? j->p_scalars : j->scalars.data();
+  j->rc = msm_compute(pts, sc, j->n, &o, j->out);
 }
 
 void complete(napi_env env, napi_status, void* data) {
@@ -66,6 +73,8 @@ void complete(napi_env env, napi_status, void* data) {
     napi_set_named_property(env, err, "code", code);
     napi_reject_deferred(env, j->deferred, err);
   }
+  if (j->ref_points) napi_delete_reference(env, j->ref_points);
+  if (j->ref_scalars) napi_delete_reference(env, j->ref_scalars);
   napi_delete_async_work(env, j->work);
   delete j;
 }
@@ -111,8 +120,15 @@ napi_value ComputeMsmU32(napi_env env, napi_callback_info info) {
   }
   Job* j = new Job();
   j->n = std::min(plen / 32, slen / 8);
-  j->points.assign(pts, pts + j->n * 32);
-  j->scalars.assign(sc, sc + j->n * 8);
+  j->p_points = pts;
+  j->p_scalars = sc;
+  if (napi_create_reference(env, argv[0], 1, &j->ref_points) != napi_ok ||
+      napi_create_reference(env, argv[1], 1, &j->ref_scalars) != napi_ok) {
+    if (j->ref_points) napi_delete_reference(env, j->ref_points);
+    delete j;
+    napi_throw_error(env, nullptr, "cannot reference the input arrays");
+    return nullptr;
+  }
   j->window = argc > 2 ? get_window(env, argv[2]) : 0;
   return start_job(env, j);
 }

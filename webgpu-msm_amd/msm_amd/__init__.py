@@ -20,7 +20,9 @@ import numpy as np
 
 __all__ = [
     "MsmError", "MsmOpts", "load", "compute_msm", "compute_msm_wire", "compute_msm_device",
-    "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "compute_msm_many_device_partial", "combine_partials", "point_add_affine",
+    "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "compute_msm_many_device_partial",
+    "compute_msm_shared_device", "compute_msm_many", "compute_msm_shared", "compute_msm_cpu", "MSM_FLAG_SERIAL",
+    "combine_partials", "point_add_affine",
     "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
@@ -50,7 +52,11 @@ class MsmProfile(ctypes.Structure):
         "fixup", "bucket_reduce_1", "bucket_reduce_2", "readback", "device_total", "host_tail")] + [
         ("entries", ctypes.c_uint64), ("window_bits", ctypes.c_uint32), ("windows", ctypes.c_uint32),
         ("run_length", ctypes.c_uint32), ("chunk_len", ctypes.c_uint32),
-        ("accumulate_sum", ctypes.c_double), ("device_total_sum", ctypes.c_double), ("profiled", ctypes.c_uint32)]
+        ("accumulate_sum", ctypes.c_double), ("device_total_sum", ctypes.c_double), ("profiled", ctypes.c_uint32),
+        ("msms_per_launch", ctypes.c_uint32), ("accumulate_union_sum", ctypes.c_double)]
+
+MSM_FLAG_SERIAL = 1  # pipelined entries: one launch in flight at a time
+MSM_STREAM_NULL = 1  # hip_stream value: order after the null (legacy default) stream
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -93,6 +99,10 @@ def load() -> ctypes.CDLL:
         "msm_compute_batch_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
         "msm_compute_many_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
         "msm_compute_many_device_partial": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_compute_shared_device": ([vp, vp, sz, sz, optp, vp, u32p], ctypes.c_int),
+        "msm_compute_many": ([vp, vp, sz, sz, optp, u32p], ctypes.c_int),
+        "msm_compute_shared": ([vp, vp, sz, sz, optp, u32p], ctypes.c_int),
+        "msm_compute_cpu": ([vp, vp, sz, ctypes.c_uint32, ctypes.c_int, u32p], ctypes.c_int),
         "msm_combine_partials": ([vp, sz, u32p], ctypes.c_int),
         "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
         "msm_split": ([ctypes.c_uint32, vp, sz, u32p], ctypes.c_int),
@@ -137,8 +147,8 @@ def _out(n: int) -> Tuple[np.ndarray, ctypes.POINTER(ctypes.c_uint32)]:
     return o, o.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
 
 
-def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1):
-    return ctypes.byref(MsmOpts(int(window_size or 0), int(run_length or 0), int(device), 0))
+def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1, flags: int = 0):
+    return ctypes.byref(MsmOpts(int(window_size or 0), int(run_length or 0), int(device), int(flags)))
 
 
 def wire_to_int(words: Iterable[int]) -> int:
@@ -241,13 +251,32 @@ def _dev_ptr(t) -> int:
     return int(t.data_ptr()) if hasattr(t, "data_ptr") else int(t)
 
 
+def _stream(stream: Optional[int], *tensors) -> Optional[int]:
+    """The stream libmsm orders its work after: the caller's, or -- when any input is a torch
+    tensor -- torch's current stream on that tensor's device (so inputs written by kernels just
+    enqueued there are complete before libmsm reads them).  Raw device pointers with no stream
+    leave the ordering to the caller (None)."""
+    if stream:
+        return stream
+    for t in tensors:
+        if hasattr(t, "is_cuda") and t.is_cuda:
+            import torch
+
+            return torch.cuda.current_stream(t.device).cuda_stream or MSM_STREAM_NULL
+    return None
+
+
+def _first(xs):
+    return xs[0] if len(xs) else None
+
+
 def compute_msm_device(d_points, d_scalars, n: int, window_size: Optional[int] = None,
                        run_length: Optional[int] = None, device: int = -1, stream: int = 0) -> Tuple[int, int]:
     """Inputs already in HBM (torch tensors or raw device pointers, wire layout)."""
     L = load()
     o, op = _out(16)
     _check(L.msm_compute_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, run_length, device),
-                                stream or None, op), "msm_compute_device")
+                                _stream(stream, d_points, d_scalars), op), "msm_compute_device")
     return _xy(o)
 
 
@@ -256,7 +285,7 @@ def compute_msm_device_partial(d_points, d_scalars, n: int, window_size: Optiona
     L = load()
     o, op = _out(32)
     _check(L.msm_compute_device_partial(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, None, device),
-                                        stream or None, op), "msm_compute_device_partial")
+                                        _stream(stream, d_points, d_scalars), op), "msm_compute_device_partial")
     return o
 
 
@@ -265,12 +294,14 @@ def compute_msm_batch_device(d_points, d_scalars, n: int, count: int, window_siz
     L = load()
     o, op = _out(16 * count)
     _check(L.msm_compute_batch_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n, count,
-                                      _opts(window_size, None, device), stream or None, op), "msm_compute_batch_device")
+                                      _opts(window_size, None, device), _stream(stream, d_points, d_scalars), op),
+           "msm_compute_batch_device")
     return o.reshape(count, 16)
 
 
 def compute_msm_many_device(points_list, scalars_list, n: int, window_size: Optional[int] = None,
-                            run_length: Optional[int] = None, device: int = -1, stream: int = 0) -> np.ndarray:
+                            run_length: Optional[int] = None, device: int = -1, stream: int = 0,
+                            flags: int = 0) -> np.ndarray:
     """len(points_list) independent n-point MSMs on device-resident inputs (torch tensors or raw
     device pointers), pipelined inside libmsm: the device runs MSM b+1 while the host finishes
     MSM b.  Returns [count][16] BE words (x | y)."""
@@ -282,9 +313,82 @@ def compute_msm_many_device(points_list, scalars_list, n: int, window_size: Opti
     ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
     o, op = _out(16 * max(count, 1))
     _check(L.msm_compute_many_device(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n, count,
-                                     _opts(window_size, run_length, device), stream or None, op),
+                                     _opts(window_size, run_length, device, flags),
+                                     _stream(stream, _first(points_list), _first(scalars_list)), op),
            "msm_compute_many_device")
     return o[:16 * count].reshape(count, 16)
+
+
+def compute_msm_shared_device(d_points, scalars_list, n: int, window_size: Optional[int] = None,
+                              run_length: Optional[int] = None, device: int = -1, stream: int = 0,
+                              flags: int = 0) -> np.ndarray:
+    """Prover batch: len(scalars_list) MSMs over ONE device-resident base vector (prepared once
+    per call).  Returns [count][16] BE words."""
+    L = load()
+    count = len(scalars_list)
+    ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
+    o, op = _out(16 * max(count, 1))
+    _check(L.msm_compute_shared_device(_dev_ptr(d_points), ctypes.cast(ss, ctypes.c_void_p), n, count,
+                                       _opts(window_size, run_length, device, flags),
+                                       _stream(stream, d_points, _first(scalars_list)), op),
+           "msm_compute_shared_device")
+    return o[:16 * count].reshape(count, 16)
+
+
+def _host_list(arrs, words: int):
+    keep = [np.ascontiguousarray(_u32(a).reshape(-1, words)) for a in arrs]
+    ptrs = (ctypes.c_void_p * max(len(keep), 1))(*[a.ctypes.data for a in keep])
+    return keep, ptrs
+
+
+def compute_msm_many(points_list, scalars_list, n: int, window_size: Optional[int] = None,
+                     run_length: Optional[int] = None, device: int = -1, flags: int = 0) -> np.ndarray:
+    """len(points_list) independent n-point MSMs of HOST arrays (wire [n, 32] / [n, 8] each),
+    uploaded into libmsm's in-flight launch slots while the others compute.  [count][16]."""
+    L = load()
+    count = len(points_list)
+    if len(scalars_list) != count:
+        raise ValueError("points_list and scalars_list differ in length")
+    kp, pp = _host_list(points_list, 32)
+    ks, ss = _host_list(scalars_list, 8)
+    for a, b in zip(kp, ks):
+        if a.shape[0] < n or b.shape[0] < n:
+            raise ValueError("an input holds fewer than n points/scalars")
+    o, op = _out(16 * max(count, 1))
+    _check(L.msm_compute_many(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n, count,
+                              _opts(window_size, run_length, device, flags), op), "msm_compute_many")
+    return o[:16 * count].reshape(count, 16)
+
+
+def compute_msm_shared(points_wire, scalars_list, n: Optional[int] = None, window_size: Optional[int] = None,
+                       run_length: Optional[int] = None, device: int = -1, flags: int = 0) -> np.ndarray:
+    """Prover batch of HOST arrays: one base vector [n, 32], len(scalars_list) scalar vectors
+    [n, 8]; the base vector is uploaded and prepared once.  [count][16]."""
+    L = load()
+    pts = np.ascontiguousarray(_u32(points_wire).reshape(-1, 32))
+    n = pts.shape[0] if n is None else n
+    ks, ss = _host_list(scalars_list, 8)
+    if pts.shape[0] < n or any(b.shape[0] < n for b in ks):
+        raise ValueError("an input holds fewer than n points/scalars")
+    count = len(ks)
+    o, op = _out(16 * max(count, 1))
+    _check(L.msm_compute_shared(_ptr(pts), ctypes.cast(ss, ctypes.c_void_p), n, count,
+                                _opts(window_size, run_length, device, flags), op), "msm_compute_shared")
+    return o[:16 * count].reshape(count, 16)
+
+
+def compute_msm_cpu(points_wire, scalars_wire, window_size: Optional[int] = None,
+                    threads: int = 0) -> Tuple[int, int]:
+    """The reference's CPU-only path (cpuWorkRatio = 1, msm_end_to_end lib.rs:106-121) as
+    libmsm's own multithreaded host Pippenger (msm_compute_cpu).  Explicit; never a fallback."""
+    L = load()
+    pts = _u32(points_wire).reshape(-1, 32)
+    sc = _u32(scalars_wire).reshape(-1, 8)
+    n = min(pts.shape[0], sc.shape[0])
+    pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
+    o, op = _out(16)
+    _check(L.msm_compute_cpu(_ptr(pts), _ptr(sc), n, int(window_size or 0), int(threads), op), "msm_compute_cpu")
+    return _xy(o)
 
 
 def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_size: Optional[int] = None,
@@ -299,7 +403,8 @@ def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_si
     ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
     o, op = _out(32 * max(count, 1))
     _check(L.msm_compute_many_device_partial(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n,
-                                             count, _opts(window_size, run_length, device), stream or None, op),
+                                             count, _opts(window_size, run_length, device),
+                                             _stream(stream, _first(points_list), _first(scalars_list)), op),
            "msm_compute_many_device_partial")
     return o[:32 * count].reshape(count, 32)
 
