@@ -41,10 +41,12 @@ def test_field_ops_random():
     mul = M._test_field_op(0, A, B)
     add = M._test_field_op(1, A, B)
     sub = M._test_field_op(2, A, B)
+    k2d = M._test_field_op(3, A, B)  # fe_mul_2d: 2d * a, the point add's small-constant multiply
     for i in range(n):
         assert _from_le(mul[i]) == a[i] * b[i] % O.P
         assert _from_le(add[i]) == (a[i] + b[i]) % O.P
         assert _from_le(sub[i]) == (a[i] - b[i]) % O.P
+        assert _from_le(k2d[i]) == 6042 * a[i] % O.P
 
 
 def test_point_ops_vs_oracle(golden):

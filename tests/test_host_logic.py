@@ -88,3 +88,61 @@ m.compute_msm([{{x: 1n, y: 2n, t: 2n, z: 1n}}], [3n]).then(
   () => console.log("resolved"), (e) => console.log("rejected " + e.code));
 """
     assert _node(script).strip() == "rejected -6"
+
+
+def _red1_lane(Wm, nm, nhi, B, L, nchunks, gd):
+    """Mirror of msm_kernels.hip red1_lane (k_bucket_reduce_1's lane -> (window, chunk) map)."""
+    nmain = Wm - 1
+    lc_hi = nchunks
+    nfull = nhi if nhi else nmain
+    lc_lo = (B // 2 + L - 1) // L if nhi else nchunks
+    live = nfull * lc_hi + (nmain - nfull) * lc_lo
+    if gd < nm * live:
+        m, r = divmod(gd, live)
+        if r < nfull * lc_hi:
+            w, c = divmod(r, lc_hi)
+        else:
+            r2 = r - nfull * lc_hi
+            w, c = nfull + r2 // lc_lo, r2 % lc_lo
+        return m * Wm + w, c, True
+    dead_lo = (nmain - nfull) * (nchunks - lc_lo)
+    per = dead_lo + nchunks
+    r0 = gd - nm * live
+    if r0 >= nm * per:
+        return None
+    m, r = divmod(r0, per)
+    if r < dead_lo:
+        span = nchunks - lc_lo
+        return m * Wm + nfull + r // span, lc_lo + r % span, False
+    return m * Wm + nmain, r - dead_lo, False
+
+
+def test_red1_lane_map_is_a_bijection_live_first():
+    """Every (window, chunk) of a launch is reduced by exactly one k_bucket_reduce_1 lane, and the
+    chunks a digit can reach come first (window geometry as make_plan builds it)."""
+    for c in (4, 5, 8, 13, 14, 15, 16):
+        wm = (254 + c - 1) // c
+        q = 254 // wm
+        nhi = 254 - q * wm
+        cc = q + 1 if nhi else q
+        B = 1 << (cc - 1)
+        Wm = wm + 1
+        for nm in ((1, 2) if c < 16 else (2,)):
+            for L in ((4, 8, 9, 10, 12, 16) if c < 15 else (9, 16)):
+                nchunks = (B + L - 1) // L
+                seen, last_live = set(), True
+                for gd in range(Wm * nm * nchunks):
+                    w, ch, live = _red1_lane(Wm, nm, nhi, B, L, nchunks, gd)
+                    assert 0 <= ch < nchunks and 0 <= w < Wm * nm
+                    assert (w, ch) not in seen
+                    seen.add((w, ch))
+                    if live:
+                        assert last_live, "live chunk after a dead one"
+                    last_live = live
+                    wl = w % Wm
+                    bits = 3 if wl == Wm - 1 else (q + 1 if wl < nhi else q)
+                    reach = 1 << (bits - 1)  # buckets a digit of this window can reach
+                    if ch * L < reach and wl != Wm - 1:
+                        assert live, (c, nm, L, w, ch)
+                assert len(seen) == Wm * nm * nchunks
+                assert _red1_lane(Wm, nm, nhi, B, L, nchunks, Wm * nm * nchunks) is None

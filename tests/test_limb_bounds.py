@@ -64,6 +64,38 @@ def fe_mul(a: B, b: B) -> B:
     return N_MUL
 
 
+K2D_INT, MU2D = 6042, (1 << 284) // P
+
+
+def fe_mul_2d_exact(v: int):
+    """Bit-exact model of fp29.cuh fe_mul_2d on the normalised representation of v (< 2^254):
+    returns (limbs, value)."""
+    a = [(v >> (LB * i)) & MASK for i in range(NL - 1)] + [v >> (LB * (NL - 1))]
+    r, c = [0] * NL, 0
+    for i in range(NL - 1):
+        c = a[i] * K2D_INT + c
+        assert c < 1 << 64
+        r[i] = c & MASK
+        c >>= LB
+    c = a[NL - 1] * K2D_INT + c
+    assert c >> 20 < 1 << 32
+    q = ((c >> 20) * MU2D) >> 32
+    d = 0
+    for i in range(NL - 1):
+        d += r[i] - q * P29[i]
+        assert -(1 << 63) <= d < 1 << 63
+        r[i] = d & MASK
+        d >>= LB  # Python's >> is arithmetic, like the int64 shift
+    r[NL - 1] = d + c - q * P29[NL - 1]
+    assert 0 <= r[NL - 1] < 1 << 32
+    return r, value_of(r)
+
+
+def fe_mul_2d(a: B) -> B:
+    assert all(x <= MASK for x in a.l[:NL - 1]) and a.v < 1 << 254
+    return B.normalised(3 * P)
+
+
 def fe_add(a: B, b: B) -> B:
     return B([x + y for x, y in zip(a.l, b.l)], a.v + b.v)
 
@@ -123,7 +155,7 @@ def test_padd_bounds():
     p = q = PT
     A = fe_mul(fe_sub_u(p["Y"], p["X"]), fe_sub(q["Y"], q["X"]))
     Bv = fe_mul(fe_add(p["Y"], p["X"]), fe_add(q["Y"], q["X"]))
-    C = fe_mul(fe_mul(p["T"], q["T"]), N_MUL)
+    C = fe_mul_2d(fe_mul(p["T"], q["T"]))
     D0 = fe_mul(p["Z"], q["Z"])
     D = fe_add(D0, D0)
     E = fe_sub_u(Bv, A)
@@ -134,6 +166,30 @@ def test_padd_bounds():
     fe_mul(G, H)
     fe_mul(E, H)
     fe_mul(F, G)
+
+
+def test_mul_2d_exact_and_bounded():
+    import random
+    rnd = random.Random(11)
+    vals = [0, 1, P - 1, P, 2 * P - 1, (1 << 254) - 1, (1 << 253), (1 << 252) - 1]
+    vals += [rnd.randrange(0, 2 * P) for _ in range(20000)] + [rnd.randrange(0, 1 << 254) for _ in range(5000)]
+    # values straddling every Barrett boundary q p of 6042 v
+    for q in range(0, 6042 * 2, 97):
+        for dv in (-2, -1, 0, 1):
+            x = (q * P) // K2D_INT + dv
+            if 0 <= x < 1 << 254:
+                vals.append(x)
+    for v in vals:
+        limbs, r = fe_mul_2d_exact(v)
+        assert r % P == (K2D_INT * v) % P
+        assert 0 <= r < 3 * P
+        assert all(x <= MASK for x in limbs[:NL - 1])
+
+
+def test_quad_add_bounds():
+    # pt_add_quad: round 1 A | B | T1T2 | Z1Z2 on the four lanes, C = fe_mul_2d(T1T2) on lane 2,
+    # then EF | GH | EH | FG -- the same operands as pt_add
+    test_padd_bounds()
 
 
 def test_pdbl_bounds():
@@ -179,13 +235,14 @@ REVIEWED = {
     ("fp29.cuh", "fe_sub"): "ea72835f159885cc",
     ("fp29.cuh", "fe_sub_u"): "3dba987a0530b5b5",
     ("fp29.cuh", "fe_neg"): "a754b1a94a6b8415",
+    ("fp29.cuh", "fe_mul_2d"): "b9f5c6afdcbc7ff4",
     ("fp29.cuh", "P29"): "b4babf5a3c9d7331",
     ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
     ("ec.cuh", "pt_madd"): "bca5cd1691b5dc73",
-    ("ec.cuh", "pt_add"): "f730177c97e49172",
+    ("ec.cuh", "pt_add"): "8b71b3f9aba1c9c2",
     ("ec.cuh", "pt_dbl"): "784353f9934ef437",
     ("ec.cuh", "pre_neg_if"): "a318c90204dc7c80",
-    ("ec.cuh", "pt_add_quad"): "917a5a92a88578ac",
+    ("ec.cuh", "pt_add_quad"): "2c7df2e0c3aa2b85",
 }
 
 

@@ -5,10 +5,14 @@ issue cycles it demands per wave-iteration on gfx950.
 
 Compiles libmsm's device code with --save-temps into a scratch directory, takes the basic block
 of k_accumulate holding the most v_mad_u64_u32 (one pt_madd per wave-iteration), and prices it
-with the issue costs measured by tools/ubench/isa_rates.hip (profiles/r2_isa_rates.json): a
-SIMD-32 issues a 32-bit VALU wave64 instruction in 2 cycles and a 64-bit one (v_mad_u64_u32,
-64-bit shifts/adds/moves) in 4.  bench.py turns cycles_per_iteration into the ISA roofline:
-frac_isa = (entries / 64) * cycles_per_iteration / (k_accumulate seconds * SIMDs * clock).
+two ways:
+  * cycles_per_iteration: the nominal gfx950 model (a SIMD-32 issues a 32-bit VALU wave64
+    instruction in 2 cycles, a 64-bit one -- v_mad_u64_u32, 64-bit shifts/adds/moves -- in 4);
+  * ns_per_iteration_chip: every instruction at the chip-wide issue rate MEASURED for it (or its
+    encoding class) by tools/ubench/isa_rates.hip (profiles/r2_isa_rates.json, G wave-instructions
+    per second over all 256 CUs), so clock and encoding effects are in the price.
+bench.py turns these into the ISA floor of the kernel: floor = (entries / 64) x ns_per_iteration_chip,
+frac_isa_measured = floor / k_accumulate duration.
 """
 import argparse
 import collections
@@ -52,6 +56,37 @@ def blocks_of(asm, func):
     return out, loops
 
 
+# instructions the rate benchmark does not time, priced as the measured instruction of their
+# encoding class (VOP2 32-bit ~ v_and_b32, VOP3 32-bit ~ v_add3_u32, 64-bit shifts ~ v_lshrrev_b64)
+RATE_CLASS = {"v_sub_u32": "v_add_u32", "v_add_u32": "v_add_u32", "v_lshrrev_b32": "v_and_b32",
+              "v_lshlrev_b32": "v_and_b32", "v_or_b32": "v_and_b32", "v_xor_b32": "v_and_b32",
+              "v_mov_b32": "v_and_b32", "v_not_b32": "v_and_b32", "v_bitop3_b32": "v_add3_u32",
+              "v_bfi_b32": "v_add3_u32", "v_lshl_or_b32": "v_add3_u32", "v_and_or_b32": "v_add3_u32",
+              "v_or3_b32": "v_add3_u32", "v_lshlrev_b64": "v_lshrrev_b64", "v_ashrrev_i64": "v_lshrrev_b64",
+              "v_add_co_u32": "v_and_b32", "v_addc_co_u32": "v_and_b32", "v_sub_co_u32": "v_and_b32",
+              "v_subb_co_u32": "v_and_b32", "v_perm_b32": "v_add3_u32", "v_mul_lo_u32": "v_mul_lo_u32",
+              "v_mul_hi_u32": "v_mul_hi_u32"}
+
+
+def price_measured(cnt, rates_path):
+    """Chip-wide ns per wave-iteration (one wave of every SIMD... i.e. per 1 wave-instruction
+    stream) from the measured issue rates; returns (ns, unpriced ops)."""
+    with open(rates_path) as f:
+        rates = json.load(f)["rates"]
+    ns, unpriced = 0.0, {}
+    for op, c in cnt.items():
+        if not op.startswith("v_"):
+            continue  # scalar / memory / waitcnt: not VALU issue
+        key = op if op in rates else RATE_CLASS.get(op)
+        if key is None and op.startswith("v_cmp"):
+            key = "v_and_b32"
+        if key is None or key not in rates:
+            unpriced[op] = c
+            key = "v_add3_u32"
+        ns += c / rates[key]["G_wave_inst_per_s"]  # G/s -> ns per wave-instruction, chip-wide
+    return ns, unpriced
+
+
 def base(op):
     return re.sub(r"_e(32|64)$", "", op)
 
@@ -60,6 +95,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_isa_mix.json"))
     ap.add_argument("--func", default="k_accumulate")
+    ap.add_argument("--rates", default=os.path.join(ROOT, "profiles", "r2_isa_rates.json"))
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         blocks, loops = blocks_of(asm_text(tmp), args.func)
@@ -77,6 +113,15 @@ def main():
            "cycle_model": "gfx950 SIMD-32: 2 cycles per 32-bit VALU wave64 instruction, 4 per 64-bit one "
                           "(v_mad_u64_u32, 64-bit shifts/adds/moves); profiles/r2_isa_rates.json",
            "mix": dict(cnt.most_common())}
+    if os.path.exists(args.rates):
+        ns, unpriced = price_measured(cnt, args.rates)
+        res["ns_per_iteration_chip"] = ns
+        res["rates_file"] = os.path.relpath(args.rates, ROOT)
+        res["measured_model"] = ("sum over the block's VALU instructions of 1 / (chip-wide measured issue rate of the "
+                                 "instruction or its encoding class): ns of chip time per wave-iteration when every "
+                                 "SIMD issues back to back")
+        if unpriced:
+            res["unpriced_as_vop3"] = unpriced
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "mix"}))

@@ -8,7 +8,7 @@
 // them.  Prints one JSON line: median and all run times (ms), and whether every result matched.
 import fs from "fs";
 import { performance } from "perf_hooks";
-import { compute_msm } from "../webgpu-msm_amd/js/submission.mjs";
+import { compute_msm, flattenU32 } from "../webgpu-msm_amd/js/submission.mjs";
 
 const [, , pPath, sPath, nArg, runsArg, xArg, yArg] = process.argv;
 const n = parseInt(nArg, 10);
@@ -39,8 +39,16 @@ const expect = xArg ? { x: BigInt(xArg), y: BigInt(yArg) } : null;
     if (r > 0) times.push(t1 - t0); // run 0 warms the addon, device context and graphs
     if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
   }
-  const sorted = [...times].sort((a, b) => a - b);
-  console.log(JSON.stringify({ node_e2e_ms: sorted[Math.floor(sorted.length / 2)], runs_ms: times, correct: expect ? ok : null }));
+  // the JS marshalling share alone: compute_msm's flatten of the U32ArrayPoint[] objects
+  const flat = [];
+  for (let r = 0; r < runs; r++) {
+    const t0 = performance.now();
+    flattenU32(points, scalars);
+    flat.push(performance.now() - t0);
+  }
+  const med = (xs) => [...xs].sort((a, b) => a - b)[Math.floor(xs.length / 2)];
+  console.log(JSON.stringify({ node_e2e_ms: med(times), marshal_ms: med(flat), runs_ms: times,
+                               correct: expect ? ok : null }));
 })().catch((e) => {
   console.log(JSON.stringify({ error: String(e) }));
   process.exit(1);

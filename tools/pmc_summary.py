@@ -66,17 +66,16 @@ def main():
     if acc and n:
         fetch = acc.get("FETCH_SIZE_per_unit", 0) * 1024
         write = acc.get("WRITE_SIZE_per_unit", 0) * 1024
-        tr = {"n": n, "kernel": "k_accumulate",
-              "accumulate_fetch_bytes_per_msm": fetch,
+        tr = {"n": n, "kernel": "k_accumulate", "source": os.path.basename(os.path.normpath(d)),
+              "accumulate_fetch_size_bytes_per_msm": fetch,
               "accumulate_write_bytes_per_msm": write,
-              "accumulate_hbm_bytes_per_msm": fetch + write,
-              "accumulate_fetch_x2_upper_bound_per_msm": 2 * fetch,
-              "note": "FETCH_SIZE + WRITE_SIZE of k_accumulate per MSM (separate rocprofv3 --pmc passes; "
-                      "a launch carrying a batch of MSMs is counted per MSM by its grid size). Raw: the "
-                      "guide's x2 FETCH correction is for 16-B/lane coalesced streaming reads, while this "
-                      "kernel gathers 112 B of a 128-B point record per sorted entry (x2 kept as an upper "
-                      "bound). Counted at the L2's fabric side: includes Infinity-Cache hits (the 128 MiB "
-                      "point table stays resident in the 256 MiB Infinity Cache)."}
+              "accumulate_hbm_bytes_per_msm": 2 * fetch + write,
+              "note": "2 x FETCH_SIZE + WRITE_SIZE of k_accumulate per MSM (separate rocprofv3 --pmc passes; "
+                      "a launch carrying a batch of MSMs is counted per MSM by its grid size). FETCH_SIZE is "
+                      "doubled as MI355X_MICROARCH.md prescribes for 16-B/lane reads on gfx950 (the kernel "
+                      "gathers each 112-B point record with 16-B/lane loads). Counted at the L2's fabric side: "
+                      "includes Infinity-Cache hits (the 128 MiB point table stays resident in the 256 MiB "
+                      "Infinity Cache), so it is an upper bound on HBM bytes."}
     print(json.dumps({"kernels": rows, "traffic": tr}, indent=1))
     if tr and len(sys.argv) > 3:  # traffic file read by bench.py
         with open(sys.argv[3], "w") as f:

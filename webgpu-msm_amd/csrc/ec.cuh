@@ -48,11 +48,11 @@ __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
   return r;
 }
 
-// p + q, both extended projective.  add-2008-hwcd-3, k = 2d: 9M.
+// p + q, both extended projective.  add-2008-hwcd-3, k = 2d: 9M (the k multiply is fe_mul_2d).
 __device__ __forceinline__ xyzt pt_add(const xyzt& p, const xyzt& q) {
   fe A = fe_mul(fe_sub_u(p.Y, p.X), fe_sub(q.Y, q.X));  // U*N
   fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));  // S*S
-  fe C = fe_mul(fe_mul(p.T, q.T), fe_const(K2D29));
+  fe C = fe_mul_2d(fe_mul(p.T, q.T));  // k = 2d = 6042: scaled, not multiplied (value < 3p)
   fe D = fe_mul(p.Z, q.Z);
   D = fe_add(D, D);  // 2N, unnormalised (see pt_madd)
   fe E = fe_sub_u(B, A);
@@ -116,10 +116,10 @@ __device__ __forceinline__ xyzt pt_sel(bool c, const xyzt& a, const xyzt& b) {
 // ---- quad-cooperative addition (latency-bound reductions) -------------------------------------
 // Lane q = lane & 3 of each group of 4 lanes holds coordinate q (0 X, 1 Y, 2 T, 3 Z) of P in `p`
 // and of Q in `r`; every lane gets its coordinate of P + Q.  Same add-2008-hwcd-3 formula as
-// pt_add, but its 9 multiplies run as 3 rounds of one multiply per lane (A | B | T1T2 | Z1Z2, then
-// C = 2d T1T2, then EF | GH | EH | FG), operands exchanged with DPP quad permutes.  Three
-// multiply latencies instead of nine: for reduction trees whose levels are too narrow to fill
-// the machine.
+// pt_add, but its multiplies run as rounds of one multiply per lane (A | B | T1T2 | Z1Z2, then
+// C = 2d T1T2 by fe_mul_2d on lane 2, then EF | GH | EH | FG), operands exchanged with DPP quad
+// permutes.  Two multiply latencies (plus a small scaling) instead of nine: for reduction trees
+// whose levels are too narrow to fill the machine.
 template <int K>
 __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
   fe r;
@@ -136,7 +136,7 @@ __device__ __forceinline__ fe pt_add_quad(const fe& p, const fe& r) {
   fe a = fe_sel(q == 0, fe_sel(q == 1, p, a1), s1);
   fe b = fe_sel(q == 0, fe_sel(q == 1, r, a2), s2);
   const fe m = fe_mul(a, b);  // lane 0: A, 1: B, 2: T1 T2, 3: Z1 Z2
-  const fe m2 = fe_mul(m, fe_sel(q == 2, fe_one(), fe_const(K2D29)));  // lane 2: C = 2d T1 T2
+  const fe m2 = q == 2 ? fe_mul_2d(m) : m;  // lane 2: C = 2d T1 T2
   const fe A = fe_quad_bcast<0>(m2), B = fe_quad_bcast<1>(m2);
   const fe C = fe_quad_bcast<2>(m2), D0 = fe_quad_bcast<3>(m2);
   const fe D = fe_add(D0, D0);

@@ -118,11 +118,10 @@ struct HostBuf {
 struct Plan {
   MsmDims d;
   uint32_t K;       // run length
-  uint32_t L;       // bucket-reduce chunk length
-  uint32_t lgL;
-  uint32_t nchunks; // B / L
+  uint32_t L;       // bucket-reduce chunk length (any of RED1_LS; not necessarily a power of two)
+  uint32_t nchunks; // ceil(B / L)
   uint32_t nv;      // V-slices: R_V = sum_c U_c is split into nv equal partial sums
-  uint32_t nterms;  // nv + log2(nchunks)
+  uint32_t nterms;  // nv + bits of the largest chunk index
   size_t Mmax;      // W * n upper bound on sorted entries
   size_t runs_max;
 };
@@ -133,7 +132,7 @@ bool plan_eq(const Plan& a, const Plan& b) {
   const MsmDims &x = a.d, &y = b.d;
   return x.n == y.n && x.c == y.c && x.B == y.B && x.W == y.W && x.Wm == y.Wm && x.nm == y.nm && x.q == y.q &&
          x.nhi == y.nhi && x.fb == y.fb && x.nbc == y.nbc && x.nbins == y.nbins && x.ch == y.ch && x.nch == y.nch &&
-         x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L && a.lgL == b.lgL &&
+         x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L &&
          a.nchunks == b.nchunks && a.nv == b.nv && a.nterms == b.nterms && a.Mmax == b.Mmax &&
          a.runs_max == b.runs_max;
 }
@@ -308,9 +307,31 @@ uint32_t pipelined_window(size_t n) {
   return msm_best_window(n);
 }
 
+// Chunk lengths k_bucket_reduce_1 is instantiated for.
+constexpr uint32_t RED1_LS[] = {8, 9, 10, 12, 16};
+
+// Buckets per k_bucket_reduce_1 lane: the shortest chain (L) for which the live lanes of every
+// MSM's main windows fit in one wave per SIMD (see msm_kernels.hip); 16 if none does.  Measured
+// (profiles/r2i_ks17*): c = 15 with two MSMs per launch ran L = 8 as 1,056 waves -- two chains on
+// some SIMDs, 140 us -- where L = 9 fits.  MSM_RED_L overrides (any of RED1_LS, or 4).
+uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
+  static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
+  if (l_env == 4) return 4;
+  for (uint32_t L : RED1_LS)
+    if (l_env == L) return L;
+  const uint32_t nmain = d.Wm - 1;
+  const uint32_t nfull = d.nhi ? d.nhi : nmain;
+  const uint64_t simds = 4ull * (uint64_t)(n_cu > 0 ? n_cu : 256);
+  for (uint32_t L : RED1_LS) {
+    const uint64_t lc_hi = (d.B + L - 1) / L, lc_lo = d.nhi ? (d.B / 2 + L - 1) / L : lc_hi;
+    const uint64_t lanes = (uint64_t)d.nm * (nfull * lc_hi + (nmain - nfull) * lc_lo);
+    if ((lanes + 63) / 64 <= simds) return L;
+  }
+  return 16;
+}
+
 int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1,
               bool shared = false) {
-  (void)n_cu;
   *pl = Plan{};
   uint32_t c = (o && o->window_bits) ? o->window_bits : pipelined ? pipelined_window(n) : msm_best_window(n);
   if (c < 4 || c > 20) return MSM_ERR_UNSUPPORTED_WINDOW;
@@ -347,17 +368,13 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   while (kauto > 16 && (size_t)d.W * n / kauto < 262144) kauto >>= 1;
   pl->K = (o && o->run_length) ? o->run_length : kauto;
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
-  static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
-  // Buckets per k_bucket_reduce_1 lane.  L = 16 halves k_bucket_reduce_2's bit-term work but
-  // doubles the running-sum chain: a throughput win only for the wide pipelined windows (2^20:
-  // -1.5% per MSM; single-MSM latency +50 us at 2^18-2^19).  tools/l_sweep.sh; MSM_RED_L overrides.
-  pl->L = (l_env == 4 || l_env == 8 || (l_env == 16 && d.B >= 32)) ? l_env
-          : (pipelined && d.B >= (1u << 15)) ? 16u : 8u;
-  pl->lgL = ilog2(pl->L);
-  pl->nchunks = d.B / pl->L;
-  // every k_bucket_reduce_2 workgroup sums at most nchunks/2 points (the R_k terms' size)
+  pl->L = bucket_reduce_L(d, n_cu);
+  pl->nchunks = (d.B + pl->L - 1) / pl->L;
+  // every k_bucket_reduce_2 workgroup sums at most pow2ceil(nchunks)/2 points (the R_k terms' size)
   pl->nv = pl->nchunks >= 2 ? 2 : 1;
-  pl->nterms = pl->nv + ilog2(pl->nchunks);
+  uint32_t cbits = 0;
+  while ((1u << cbits) < pl->nchunks) cbits++;
+  pl->nterms = pl->nv + cbits;
   pl->Mmax = (size_t)d.W * n;
   pl->runs_max = (pl->Mmax + pl->K - 1) / pl->K + 1;
   if (pl->Mmax >= (1ull << 31)) return MSM_ERR_INVALID_ARG;
@@ -491,11 +508,21 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
   if (parts & PART_ACC) {
-    hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
-                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
-                       w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                       w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
-                       w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
+    // MSM_ACC_WPC = k > 0: a persistent grid of k workgroups per CU strides over the tiles
+    static const uint32_t wpc = getenv("MSM_ACC_WPC") ? (uint32_t)atoi(getenv("MSM_ACC_WPC")) : 0u;
+    if (wpc && (size_t)c->n_cu * wpc < rgrid) {
+      hipLaunchKernelGGL(k_accumulate_persistent, dim3(c->n_cu * wpc), dim3(ACC_THREADS), 0, s, pts,
+                         w.sorted_entry.as<uint32_t>(), w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total,
+                         pl.K, d.W * d.B, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(),
+                         w.lead_open.as<uint32_t>(), w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(),
+                         w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(), rgrid);
+    } else {
+      hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
+                         w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
+                         w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                         w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
+                         w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
+    }
     mark(PH_ACCUM);
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
@@ -507,10 +534,16 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
                        w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
     mark(PH_FIXUP);
-    hipLaunchKernelGGL(pl.L == 4 ? k_bucket_reduce_1<4> : pl.L == 16 ? k_bucket_reduce_1<16> : k_bucket_reduce_1<8>,
-                       dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s,
-                       w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K, w.cross_key.as<uint32_t>(),
-                       w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(), w.red_T.as<uint32_t>());
+    auto red1 = pl.L == 4    ? k_bucket_reduce_1<4>
+                : pl.L == 9  ? k_bucket_reduce_1<9>
+                : pl.L == 10 ? k_bucket_reduce_1<10>
+                : pl.L == 12 ? k_bucket_reduce_1<12>
+                : pl.L == 16 ? k_bucket_reduce_1<16>
+                             : k_bucket_reduce_1<8>;
+    hipLaunchKernelGGL(red1, dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s,
+                       w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K, pl.nchunks,
+                       w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(),
+                       w.red_T.as<uint32_t>());
     mark(PH_RED1);
     hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
                        w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
@@ -523,28 +556,38 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   return MSM_OK;
 }
 
-// Host tail: MSM = sum_w 2^(c w) [ sum_v R_{w,v} + sum_k 2^(lgL + k) R_{w,k} ]  (Horner over bit
+// Host tail: MSM = sum_w 2^(c w) [ sum_v R_{w,v} + sum_k L 2^k R_{w,k} ]  (Horner over bit
 // positions).  Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then
 // into_affine.  The device already emitted the terms in this file's Montgomery form
 // (fe_to_host_mont).  Runs of doublings skip T (pt_dbl_proj) except the one feeding an add.
 Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
   const MsmDims& d = pl.d;
   terms += (size_t)m * d.Wm * pl.nterms * 32;  // MSM m's windows
-  // terms in descending bit position: windows from the top, inside a window R_k from the top
-  // down to the V slices (position 0)
-  std::vector<uint32_t> pos, idx;
-  pos.reserve((size_t)d.Wm * pl.nterms);
-  idx.reserve((size_t)d.Wm * pl.nterms);
-  for (int w = (int)d.Wm - 1; w >= 0; w--)
-    for (int t = (int)pl.nterms - 1; t >= 0; t--) {
-      const uint32_t i = (uint32_t)w * pl.nterms + (uint32_t)t;
+  // (bit position, term) pairs in descending position: V slices at the window's offset, R_k once
+  // per set bit b of L at offset + k + b
+  std::vector<std::pair<uint32_t, uint32_t>> at;
+  at.reserve((size_t)d.Wm * pl.nterms * 2);
+  for (uint32_t w = 0; w < d.Wm; w++)
+    for (uint32_t t = 0; t < pl.nterms; t++) {
+      const uint32_t i = w * pl.nterms + t;
       const uint32_t* o = terms + (size_t)i * 32;
       Fq X;
       memcpy(X.l, o, 32);
       if (fq_is_zero(X) && !memcmp(o + 8, o + 24, 32)) continue;  // identity: X = 0, Y = Z
-      pos.push_back(win_off(d, (uint32_t)w) + ((uint32_t)t < pl.nv ? 0u : pl.lgL + ((uint32_t)t - pl.nv)));
-      idx.push_back(i);
+      const uint32_t off = win_off(d, w);
+      if (t < pl.nv) {
+        at.emplace_back(off, i);
+      } else {
+        for (uint32_t b = 0; (pl.L >> b) != 0; b++)
+          if ((pl.L >> b) & 1u) at.emplace_back(off + (t - pl.nv) + b, i);
+      }
     }
+  std::stable_sort(at.begin(), at.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  std::vector<uint32_t> pos(at.size()), idx(at.size());
+  for (size_t j = 0; j < at.size(); j++) {
+    pos[j] = at[j].first;
+    idx[j] = at[j].second;
+  }
   Pt acc = pt_identity();
   if (pos.empty()) return acc;
   for (size_t j = 0; j < pos.size(); j++) {
@@ -604,12 +647,13 @@ int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
   std::vector<hipGraphNode_t> nodes(num);
   if (hipGraphGetNodes(g, nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
   const void* f_acc = reinterpret_cast<const void*>(&k_accumulate);
+  const void* f_accp = reinterpret_cast<const void*>(&k_accumulate_persistent);
   hipGraphNode_t acc = nullptr;
   for (hipGraphNode_t nd : nodes) {
     hipGraphNodeType ty;
     hipKernelNodeParams kp{};
     if (hipGraphNodeGetType(nd, &ty) == hipSuccess && ty == hipGraphNodeTypeKernel &&
-        hipGraphKernelNodeGetParams(nd, &kp) == hipSuccess && kp.func == f_acc)
+        hipGraphKernelNodeGetParams(nd, &kp) == hipSuccess && (kp.func == f_acc || kp.func == f_accp))
       acc = nd;
   }
   if (!acc) return MSM_ERR_HIP;

@@ -765,25 +765,25 @@ __device__ __forceinline__ uint32_t next_nonempty(const uint32_t* __restrict__ b
 #define MSM_ACC_VEC 1
 #endif
 constexpr uint32_t ACC_THREADS = 256;
-extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
-                                                                       const uint32_t* __restrict__ sorted_entry,
-                                                                       const uint32_t* __restrict__ bucket_start,
-                                                                       const uint32_t* __restrict__ run_key,
-                                                                       const uint32_t* __restrict__ total_ptr, uint32_t K,
-                                                                       uint32_t nkeys,
-                                                                       uint32_t* __restrict__ buckets,
-                                                                       uint32_t* __restrict__ lead_val,
-                                                                       uint32_t* __restrict__ lead_open,
-                                                                       uint32_t* __restrict__ cross_key,
-                                                                       uint32_t* __restrict__ skew_list,
-                                                                       uint32_t* __restrict__ g_head,
-                                                                       uint32_t* __restrict__ g_hkey,
-                                                                       uint32_t* __restrict__ g_tkey) {
-  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
-  __shared__ uint32_t sh_hkey[ACC_THREADS];
+// One workgroup-sized tile of the accumulation: runs [wg ACC_THREADS, (wg + 1) ACC_THREADS).
+__device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WORDS], uint32_t* sh_hkey,
+                                         const uint32_t* __restrict__ pts,
+                                         const uint32_t* __restrict__ sorted_entry,
+                                         const uint32_t* __restrict__ bucket_start,
+                                         const uint32_t* __restrict__ run_key,
+                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                         uint32_t nkeys,
+                                         uint32_t* __restrict__ buckets,
+                                         uint32_t* __restrict__ lead_val,
+                                         uint32_t* __restrict__ lead_open,
+                                         uint32_t* __restrict__ cross_key,
+                                         uint32_t* __restrict__ skew_list,
+                                         uint32_t* __restrict__ g_head,
+                                         uint32_t* __restrict__ g_hkey,
+                                         uint32_t* __restrict__ g_tkey) {
   const uint32_t M = *total_ptr;
   const uint32_t lt = threadIdx.x;
-  const uint32_t t = blockIdx.x * ACC_THREADS + lt;
+  const uint32_t t = wg * ACC_THREADS + lt;
   const uint32_t s = t * K;
   sh_hkey[lt] = KEY_INVALID;
   xyzt acc = pt_identity();
@@ -846,8 +846,8 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   }
   // the last live run of the workgroup says whether a bucket leaves the workgroup
   const uint32_t nruns = (M + K - 1) / K;
-  const uint32_t last = min(ACC_THREADS, nruns - min(nruns, blockIdx.x * ACC_THREADS)) - 1;
-  if (lt == last) cross_key[blockIdx.x] = cont ? cur : KEY_INVALID;
+  const uint32_t last = min(ACC_THREADS, nruns - min(nruns, wg * ACC_THREADS)) - 1;
+  if (lt == last) cross_key[wg] = cont ? cur : KEY_INVALID;
   __syncthreads();
   // Chains of heads: a run whose head is "pass" continues into the next run.  Runs of three or
   // more pass heads in a row (buckets of ~200+ entries: skewed scalars), and a lead chain that
@@ -871,7 +871,7 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
       g_tkey[t] = has_tail ? cur : KEY_INVALID;
       if (has_tail) store_pt(buckets + (size_t)cur * PT_WORDS, acc);
     }
-    if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = blockIdx.x;
+    if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = wg;
     return;
   }
   // Lane 0's head is the end of the previous workgroup's crossing bucket: the workgroup's lead.
@@ -879,9 +879,9 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   // past the workgroup here), and lane 0 joins those heads into the lead.
   const bool lead_join = lt == 0 && my_pass;
   if (lt == 0) {
-    lead_open[blockIdx.x] = 0u;
+    lead_open[wg] = 0u;
     if (s < M && hk != KEY_INVALID && !lead_join)
-      store_pt(lead_val + (size_t)blockIdx.x * PT_WORDS, load_pt_lds(sh_head[0]));
+      store_pt(lead_val + (size_t)wg * PT_WORDS, load_pt_lds(sh_head[0]));
   }
   if (has_tail || lead_join) {
     // a tail's bucket continues in run lt+1 (and lt+2, lt+3 while those are pass-through), unless
@@ -895,7 +895,50 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
     if (nwalk) acc = pt_add(acc, load_pt_lds(sh_head[lt + 1]));
     if (nwalk > 1) acc = pt_add(acc, load_pt_lds(sh_head[lt + 2]));
     if (nwalk > 2) acc = pt_add(acc, load_pt_lds(sh_head[lt + 3]));
-    store_pt(lead_join ? lead_val + (size_t)blockIdx.x * PT_WORDS : buckets + (size_t)cur * PT_WORDS, acc);
+    store_pt(lead_join ? lead_val + (size_t)wg * PT_WORDS : buckets + (size_t)cur * PT_WORDS, acc);
+  }
+}
+
+// The kernel: one tile per workgroup.  k_accumulate_persistent (MSM_ACC_WPC = k) instead runs a
+// persistent grid of k workgroups per CU that strides over the tiles, leaving CU room for other
+// launches' kernels in flight beside it (a separate kernel: the loop costs registers).
+extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
+                                         const uint32_t* __restrict__ sorted_entry,
+                                         const uint32_t* __restrict__ bucket_start,
+                                         const uint32_t* __restrict__ run_key,
+                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                         uint32_t nkeys,
+                                         uint32_t* __restrict__ buckets,
+                                         uint32_t* __restrict__ lead_val,
+                                         uint32_t* __restrict__ lead_open,
+                                         uint32_t* __restrict__ cross_key,
+                                         uint32_t* __restrict__ skew_list,
+                                         uint32_t* __restrict__ g_head,
+                                         uint32_t* __restrict__ g_hkey,
+                                         uint32_t* __restrict__ g_tkey) {
+  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
+  __shared__ uint32_t sh_hkey[ACC_THREADS];
+  acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets, lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
+}
+extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate_persistent(const uint32_t* __restrict__ pts,
+                                         const uint32_t* __restrict__ sorted_entry,
+                                         const uint32_t* __restrict__ bucket_start,
+                                         const uint32_t* __restrict__ run_key,
+                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
+                                         uint32_t nkeys,
+                                         uint32_t* __restrict__ buckets,
+                                         uint32_t* __restrict__ lead_val,
+                                         uint32_t* __restrict__ lead_open,
+                                         uint32_t* __restrict__ cross_key,
+                                         uint32_t* __restrict__ skew_list,
+                                         uint32_t* __restrict__ g_head,
+                                         uint32_t* __restrict__ g_hkey,
+                                         uint32_t* __restrict__ g_tkey, uint32_t ntiles) {
+  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
+  __shared__ uint32_t sh_hkey[ACC_THREADS];
+  for (uint32_t wg = blockIdx.x; wg < ntiles; wg += gridDim.x) {
+    if (wg != blockIdx.x) __syncthreads();  // the previous tile's joins have read sh_head / sh_hkey
+    acc_tile(wg, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets, lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
   }
 }
 
@@ -906,15 +949,15 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
 // owner adds the chain that follows it, and lane 0 publishes the workgroup's lead.
 constexpr uint32_t CJ_GRID = 256;  // k_chain_join workgroups (they loop over the skewed list)
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uint32_t* __restrict__ skew_list,
-                                                                       const uint32_t* __restrict__ total_ptr,
-                                                                       uint32_t K,
-                                                                       const uint32_t* __restrict__ g_head,
-                                                                       const uint32_t* __restrict__ g_hkey,
-                                                                       const uint32_t* __restrict__ g_tkey,
-                                                                       uint32_t* __restrict__ buckets,
-                                                                       uint32_t* __restrict__ lead_val,
-                                                                       uint32_t* __restrict__ lead_open,
-                                                                       uint32_t* __restrict__ lead_flag) {
+                                         const uint32_t* __restrict__ total_ptr,
+                                         uint32_t K,
+                                         const uint32_t* __restrict__ g_head,
+                                         const uint32_t* __restrict__ g_hkey,
+                                         const uint32_t* __restrict__ g_tkey,
+                                         uint32_t* __restrict__ buckets,
+                                         uint32_t* __restrict__ lead_val,
+                                         uint32_t* __restrict__ lead_open,
+                                         uint32_t* __restrict__ lead_flag) {
   const uint32_t nskew = skew_list[0];
   if (blockIdx.x >= nskew) return;
   const uint32_t M = *total_ptr;
@@ -1026,41 +1069,82 @@ extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* _
 // ---------------------------------------------------------------------------------------------
 // bucket reduction:  G_w = sum_{b} (b+1) B_{w,b}
 //   chunk c (L buckets): U_c = sum_i (i+1) B_{cL+i}, T_c = sum_i B_{cL+i}   (running sums)
-//   G_w = sum_c U_c + L * sum_c c T_c = R_{w,V} + sum_k 2^(lgL+k) R_{w,k},  R_{w,k} = sum_{c: bit k} T_c
+//   G_w = sum_c U_c + L * sum_c c T_c = R_{w,V} + sum_k L 2^k R_{w,k},  R_{w,k} = sum_{c: bit k} T_c
+// L need not be a power of two: the host Horner places R_{w,k} once per set bit of L.
 // ---------------------------------------------------------------------------------------------
-// L = buckets per k_bucket_reduce_1 lane (8; c >= 4 gives B >= 8).  L = 4 halves each lane's
-// running-sum chain but doubles the R_k trees of k_bucket_reduce_2: measured no faster at any
-// size, so it is only an experiment switch (MSM_RED_L=4).
+// L = buckets per k_bucket_reduce_1 lane.  Each lane's running sums are a chain of ~2L dependent
+// adds and one wave per SIMD already keeps its VALU ~82% busy, so the kernel takes ~one chain per
+// SIMD -- as long as the live lanes fit in one wave per SIMD.  The host picks the smallest L
+// (of RED1_LS) for which they do (bucket_reduce_L): at c = 15 two MSMs have 540,672 live buckets,
+// so L = 8 would need 1,056 waves on 1,024 SIMDs (two chains on some) and L = 9 needs 939.
 #ifndef MSM_RED1_THREADS
 #define MSM_RED1_THREADS 256
 #endif
 constexpr uint32_t RED1_THREADS = MSM_RED1_THREADS;
+
+// Lane -> (window, chunk) of k_bucket_reduce_1.  Live chunks (those holding buckets a digit of
+// their window can reach) of every MSM's main windows come first, so real work is whole waves at
+// the front of the grid; then the empty ones: the upper halves of (q)-bit windows in a
+// (q+1)-bit table, and the overflow windows (empty for canonical scalars).
+__device__ __forceinline__ bool red1_lane(const MsmDims& d, uint32_t L, uint32_t nchunks, uint32_t gd, uint32_t& w,
+                                          uint32_t& c) {
+  const uint32_t nmain = d.Wm - 1;
+  const uint32_t lc_hi = nchunks;                                // (c)-bit windows: every chunk live
+  const uint32_t nfull = d.nhi ? d.nhi : nmain;                  // windows of the table's full width
+  const uint32_t lc_lo = d.nhi ? (d.B / 2 + L - 1) / L : nchunks;  // (c-1)-bit windows
+  const uint32_t live = nfull * lc_hi + (nmain - nfull) * lc_lo;  // per MSM
+  if (gd < d.nm * live) {
+    const uint32_t m = gd / live, r = gd % live;
+    if (r < nfull * lc_hi) {
+      w = r / lc_hi;
+      c = r % lc_hi;
+    } else {
+      const uint32_t r2 = r - nfull * lc_hi;
+      w = nfull + r2 / lc_lo;
+      c = r2 % lc_lo;
+    }
+    w += m * d.Wm;
+    return true;
+  }
+  // dead region: per MSM, (nmain - nfull) windows x (nchunks - lc_lo) empty chunks, then the
+  // overflow window's nchunks chunks
+  const uint32_t dead_lo = (nmain - nfull) * (nchunks - lc_lo);
+  const uint32_t per = dead_lo + nchunks;
+  const uint32_t r0 = gd - d.nm * live;
+  if (r0 >= d.nm * per) return false;
+  const uint32_t m = r0 / per, r = r0 % per;
+  if (r < dead_lo) {
+    const uint32_t span = nchunks - lc_lo;
+    w = m * d.Wm + nfull + r / span;
+    c = lc_lo + r % span;
+  } else {
+    w = m * d.Wm + nmain;
+    c = r - dead_lo;
+  }
+  return true;
+}
+
 template <uint32_t RL>
 __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
                                                          const uint32_t* __restrict__ bucket_start, MsmDims d,
-                                                         uint32_t K, const uint32_t* __restrict__ cross_key,
+                                                         uint32_t K, uint32_t nchunks,
+                                                         const uint32_t* __restrict__ cross_key,
                                                          const uint32_t* __restrict__ lead_val,
                                                          uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
-  const uint32_t nchunks = d.B / RL;
-  const uint32_t gd = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gd >= d.W * nchunks) return;
-  // Dispatch order: every MSM's main windows first, the overflow windows (empty for canonical
-  // scalars: their lanes return at once) last.  The real work is then exactly 1 (L = 16) or 2
-  // (L = 8) waves per SIMD at 2^20 instead of spilling a tail round onto a few CUs.
-  const uint32_t wd = gd / nchunks, c = gd % nchunks;
-  const uint32_t nmain = d.nm * (d.Wm - 1);
-  const uint32_t w = wd < nmain ? (wd / (d.Wm - 1)) * d.Wm + wd % (d.Wm - 1) : (wd - nmain) * d.Wm + d.Wm - 1;
+  uint32_t w, c;
+  if (!red1_lane(d, RL, nchunks, blockIdx.x * blockDim.x + threadIdx.x, w, c)) return;
   const uint32_t g = w * nchunks + c;
   const uint32_t key0 = w * d.B + c * RL;
+  const uint32_t nb = min(RL, d.B - c * RL);  // buckets of this chunk inside the window (last chunk: fewer)
   // bucket metadata up front (independent loads): which buckets are non-empty, and which left
   // their accumulation workgroup and need the continuation from lead_val
   uint32_t bs[RL + 1];
 #pragma unroll
-  for (uint32_t i = 0; i <= RL; i++) bs[i] = bucket_start[key0 + i];
+  for (uint32_t i = 0; i <= RL; i++) bs[i] = i <= nb ? bucket_start[key0 + i] : 0u;
   uint32_t live = 0, cross = 0;
 #pragma unroll
   for (uint32_t i = 0; i < RL; i++) {
-    if (bs[i + 1] != bs[i]) {
+    if (i < nb && bs[i + 1] != bs[i]) {
       live |= 1u << i;
       if (cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
     }
@@ -1077,13 +1161,13 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
   // current bucket's adds.  (Interleaving the two adds of a step for ILP costs more in VGPRs and
   // spills than it gains here: measured.)
   int i = 31 - __builtin_clz(live);
-  xyzt nb = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
+  xyzt nb_pt = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
 #pragma unroll 1
   for (; i >= 0; i--) {
     if ((live >> i) & 1u) {
-      xyzt b = nb;
+      xyzt b = nb_pt;
       const uint32_t below = live & ((1u << i) - 1u);
-      if (below) nb = load_pt(buckets + (size_t)(key0 + 31 - __builtin_clz(below)) * PT_WORDS);
+      if (below) nb_pt = load_pt(buckets + (size_t)(key0 + 31 - __builtin_clz(below)) * PT_WORDS);
       if ((cross >> i) & 1u) {  // rare: reload the bucket's start rather than index bs[] dynamically
         const uint32_t g0 = (bucket_start[key0 + i] / K) / ACC_THREADS;
         b = pt_add(b, load_pt(lead_val + (size_t)(g0 + 1) * PT_WORDS));
@@ -1101,7 +1185,8 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
 }
 
 // One workgroup per (window, term).  Terms 0..nv-1: R_{V,v} = sum of U_c over the v-th slice of
-// chunks; term nv+k: R_k = sum_{c: bit k of c} T_c.  Every workgroup sums at most nchunks/2 points.
+// chunks; term nv+k: R_k = sum_{c: bit k of c} T_c.  Every workgroup sums at most
+// pow2ceil(nchunks)/2 points.
 // Output: X, Y, T, Z in the host's Montgomery form (a * 2^256 mod p, 8 LE words each), written
 // straight into coherent pinned host memory (no readback copy), so the host Horner
 // (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
@@ -1128,14 +1213,18 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
   const bool vterm = term < nv;
   const uint32_t* src = vterm ? in_U : in_T;
   const uint32_t kbit = term - nv;
-  // Every term sums exactly nchunks/2 points (a V slice, or the chunks with bit k set), and the
-  // j-th of them is enumerated directly, so every lane loads the same number of points (a
-  // stride-and-skip loop over all chunks would give half the lanes all the work for k < 10).
-  const uint32_t half_n = nchunks / 2;
+  // A V slice is ceil(nchunks/nv) consecutive chunks; a bit term enumerates its j-th chunk with
+  // bit k set directly (j < pow2ceil(nchunks)/2, chunks past the end skipped), so every lane
+  // loads about the same number of points (a stride-and-skip loop over all chunks would give half
+  // the lanes all the work for k < 10).
+  const uint32_t vslice = (nchunks + nv - 1) / nv;
+  uint32_t half_n = 1;
+  while (2 * half_n < nchunks) half_n <<= 1;
   xyzt acc = pt_identity();
   bool live = false;
-  for (uint32_t j = threadIdx.x; j < (nv == 1 && vterm ? nchunks : half_n); j += RED2_THREADS) {
-    const uint32_t c = vterm ? term * half_n + j : (((j >> kbit) << (kbit + 1)) | (1u << kbit) | (j & ((1u << kbit) - 1u)));
+  for (uint32_t j = threadIdx.x; j < (vterm ? vslice : half_n); j += RED2_THREADS) {
+    const uint32_t c = vterm ? term * vslice + j : (((j >> kbit) << (kbit + 1)) | (1u << kbit) | (j & ((1u << kbit) - 1u)));
+    if (c >= nchunks) continue;
     xyzt p = load_pt(src + ((size_t)w * nchunks + c) * PT_WORDS);
     acc = live ? pt_add(acc, p) : p;
     live = true;
@@ -1184,7 +1273,7 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
 }
 
 // Small utility kernels used by tests: batch field ops / point ops on canonical inputs.
-// op 0: field mul, 1: add, 2: sub; inputs LE standard words [n][8] x2, output [n][8].
+// op 0: field mul, 1: add, 2: sub, 3: 2d * a (fe_mul_2d); inputs LE standard words [n][8] x2, output [n][8].
 extern "C" __global__ void k_test_field(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                                         uint32_t* __restrict__ out, uint32_t n, uint32_t op) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1196,7 +1285,7 @@ extern "C" __global__ void k_test_field(const uint32_t* __restrict__ a, const ui
     bw[k] = b[(size_t)i * 8 + k];
   }
   fe x = fe_to_mont(fe_from_words_le(aw)), y = fe_to_mont(fe_from_words_le(bw));
-  fe r = op == 0 ? fe_mul(x, y) : op == 1 ? fe_add_n(x, y) : fe_sub(x, y);
+  fe r = op == 0 ? fe_mul(x, y) : op == 1 ? fe_add_n(x, y) : op == 2 ? fe_sub(x, y) : fe_mul_2d(x);
   fe_to_words_le(fe_to_std(r), ow);
 #pragma unroll
   for (int k = 0; k < 8; k++) out[(size_t)i * 8 + k] = ow[k];

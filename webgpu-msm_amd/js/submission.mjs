@@ -42,7 +42,8 @@ export function u32ArrayToBigInts(u32Array) {
 }
 
 // U32ArrayPoint[] / Uint32Array[] -> flat wire buffers (submission.ts:75-86 layout x|y|t|z).
-function flattenU32(points, scalars) {
+// Exported for tools/node_e2e.mjs, which times this JS marshalling share of compute_msm.
+export function flattenU32(points, scalars) {
   const n = Math.min(points.length, scalars.length);
   const pointBuffer = new Uint32Array(n * nUint32PerPoint);
   const scalarBuffer = new Uint32Array(n * nUint32PerScalar);
