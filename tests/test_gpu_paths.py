@@ -34,6 +34,19 @@ def test_host_entry_ragged_pieces():
     assert M.compute_msm_wire(pts[:n2], sc[:n2]) == closed_form(5, 3, sc[:n2])
 
 
+@pytest.mark.parametrize("n", [2 * (1 << 17), 3 * (1 << 17) + 2, (1 << 19) + 7])
+def test_host_entry_split_into_slices(n):
+    # msm_compute from host arrays at n >= 2^18 runs G point-slices through the pipelined entry
+    # (slice g+1 uploads while slice g computes) and joins the partials; n not a multiple of G
+    # leaves a remainder MSM of < G points
+    pts = M.gen_points(n, k0=3, step=5)
+    sc = M.gen_scalars(n, seed=41 + n % 7)
+    exp = closed_form(3, 5, sc)
+    assert M.compute_msm_wire(pts, sc) == exp
+    part = M.compute_msm_partial(pts, sc)
+    assert M.combine_partials(np.asarray(part, dtype=np.uint32).reshape(1, 32)) == exp
+
+
 def test_host_many_distinct():
     cases = []
     for j, n in enumerate((3000, 3000, 3000, 3000, 3000)):

@@ -1116,6 +1116,7 @@ struct ManyInputs {
   const uint32_t* const* points = nullptr;  // per MSM (ignored when shared_points is set)
   const uint32_t* const* scalars = nullptr;
   const uint32_t* shared_points = nullptr;  // one base vector for every MSM (prover batch)
+  uint32_t batch = 0;                        // MSMs per launch (0: pipeline_batch's choice)
 };
 
 // `count` MSMs of n points each, pipelined over pipeline_slots slots, each with its own stream and
@@ -1128,9 +1129,11 @@ struct ManyInputs {
 // once, before the first launch, and every launch reads its records.  Results go out affine (16
 // words each) or, with `projective`, as X|Y|T|Z partials (32 words).
 int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_opts* o, hipStream_t user_stream,
-             uint32_t* out_be, bool projective) {
+             uint32_t* out_be, bool projective, Pt* out_pts = nullptr) {
   auto emit = [&](const Pt& r, size_t b) {
-    if (projective)
+    if (out_pts)
+      out_pts[b] = r;
+    else if (projective)
       pt_to_be_xyzt(r, out_be + 32 * b);
     else
       pt_to_be_affine(r, out_be + 16 * b);
@@ -1143,7 +1146,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   const bool host = in.kind == ManyInputs::HOST;
   for (size_t b = 0; b < count; b++)
     if ((!shared && !in.points[b]) || !in.scalars[b]) return MSM_ERR_INVALID_ARG;
-  const uint32_t nm = pipeline_batch(n, count);
+  const uint32_t nm = in.batch ? (uint32_t)std::min<size_t>(in.batch, count) : pipeline_batch(n, count);
   const size_t nbatch = (count + nm - 1) / nm;
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm, shared);
@@ -1267,9 +1270,55 @@ int on_device(const msm_opts* opts, F&& fn) {
   return rc;
 }
 
+// Host-input points per slice of a split MSM (run_host_split), and MSMs per launch there.
+size_t host_piece() {
+  static const size_t v = getenv("MSM_HOST_PIECE_LOG") ? (size_t)1 << atoi(getenv("MSM_HOST_PIECE_LOG")) : (size_t)1 << 17;
+  return v;
+}
+uint32_t host_batch() {
+  static const uint32_t v = getenv("MSM_HOST_NM") ? (uint32_t)atoi(getenv("MSM_HOST_NM")) : 0u;
+  return v;
+}
+
+// One large MSM of host-resident inputs as G point-slices (G <= 16, slices of >= 2^17 points):
+// MSM = sum_g MSM(slice g), the reference's own shard/join identity (submission.ts:116-154,
+// lib.rs:240-253) inside one GPU.  The slices go through the pipelined entry: slice g+1 uploads
+// on the copy stream while slice g runs, so the PCIe transfer -- the bulk of a host-input MSM --
+// overlaps all the compute but the last launch's; the partials are joined with G - 1 adds.  A
+// remainder of fewer than G points (n not a multiple of G) is one more small MSM.
+int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
+                   Pt* result) {
+  const size_t G = std::min<size_t>(16, n / host_piece());
+  const size_t s = n / G, done = G * s;
+  std::vector<const uint32_t*> pp(G), ss(G);
+  for (size_t g = 0; g < G; g++) {
+    pp[g] = points_be + g * s * 32;
+    ss[g] = scalars_be + g * s * 8;
+  }
+  ManyInputs in;
+  in.kind = ManyInputs::HOST;
+  in.points = pp.data();
+  in.scalars = ss.data();
+  in.batch = host_batch();
+  std::vector<Pt> part(G + 1, pt_identity());
+  int rc = run_many(c, in, s, G, o, nullptr, nullptr, true, part.data());
+  if (rc != MSM_OK) return rc;
+  if (done < n && (rc = run_host(c, points_be + done * 32, scalars_be + done * 8, n - done, o, &part[G])) != MSM_OK)
+    return rc;
+  Pt acc = part[0];
+  for (size_t g = 1; g <= G; g++) acc = pt_add(acc, part[g]);
+  *result = acc;
+  return MSM_OK;
+}
+
 int host_entry(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts, Pt* r) {
   if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
-  return on_device(opts, [&](DevCtx* c) { return run_host(c, points_be, scalars_be, n, opts, r); });
+  static const bool split_off = getenv("MSM_HOST_SPLIT") && atoi(getenv("MSM_HOST_SPLIT")) == 0;
+  return on_device(opts, [&](DevCtx* c) {
+    if (!split_off && n >= 2 * host_piece())
+      return run_host_split(c, points_be, scalars_be, n, opts, r);
+    return run_host(c, points_be, scalars_be, n, opts, r);
+  });
 }
 
 int device_entry(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
