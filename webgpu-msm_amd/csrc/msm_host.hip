@@ -20,6 +20,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/msm.h"
@@ -308,12 +309,13 @@ uint32_t pipelined_window(size_t n) {
 }
 
 // Chunk lengths k_bucket_reduce_1 is instantiated for.
-constexpr uint32_t RED1_LS[] = {8, 9, 10, 12, 16};
+constexpr uint32_t RED1_LS[] = {8, 9, 10, 12, 16, 17, 20};
 
 // Buckets per k_bucket_reduce_1 lane: the shortest chain (L) for which the live lanes of every
 // MSM's main windows fit in one wave per SIMD (see msm_kernels.hip); 16 if none does.  Measured
 // (profiles/r2i_ks17*): c = 15 with two MSMs per launch ran L = 8 as 1,056 waves -- two chains on
-// some SIMDs, 140 us -- where L = 9 fits.  MSM_RED_L overrides (any of RED1_LS, or 4).
+// some SIMDs, 140 us -- where L = 9 fits.  Chains past 16 serve the four-MSM launches of small
+// sizes (2^17: L = 17, 994 waves).  MSM_RED_L overrides (any of RED1_LS, or 4).
 uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
   static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
   if (l_env == 4) return 4;
@@ -539,6 +541,8 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                 : pl.L == 10 ? k_bucket_reduce_1<10>
                 : pl.L == 12 ? k_bucket_reduce_1<12>
                 : pl.L == 16 ? k_bucket_reduce_1<16>
+                : pl.L == 17 ? k_bucket_reduce_1<17>
+                : pl.L == 20 ? k_bucket_reduce_1<20>
                              : k_bucket_reduce_1<8>;
     hipLaunchKernelGGL(red1, dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s,
                        w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K, pl.nchunks,
@@ -1102,11 +1106,13 @@ int pipeline_slots(size_t n, const msm_opts* o) {
 // MSMs per launch (batch) for the pipelined entries: the latency-bound kernels (reduction trees,
 // scans, small sorts) of two MSMs fill the machine together.  Measured on MI355X
 // (tools/batch_sweep.sh, ms per MSM, batch 1 -> 2): 2^16 0.218 -> 0.162, 2^17 0.273 -> 0.247,
-// 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136; 4 is no better than 2.
-// MSM_BATCH overrides (1..MSM_MAX_BATCH).
+// 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136.  Four per launch up to 2^17,
+// measured once the reduction kept one wave per SIMD (profiles/r2mn_*): 2^17 0.268 -> 0.248 ms
+// per MSM; at 2^18 within 1% of two.  MSM_BATCH overrides (1..MSM_MAX_BATCH).
 uint32_t pipeline_batch(size_t n, size_t count) {
   static const int env = getenv("MSM_BATCH") ? atoi(getenv("MSM_BATCH")) : 0;
-  uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH) : (n <= (1u << 20) ? 2u : 1u);
+  uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH)
+                         : (n <= (1u << 17) ? 4u : n <= (1u << 20) ? 2u : 1u);
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
@@ -1231,8 +1237,17 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       if ((rc = launch_parts(c, pl, bp, bs, si, parts, shared ? pts_shared : sl.ws.pts.as<uint32_t>())) != MSM_OK)
         return fail(rc);
     }
-    if (have)
-      for (uint32_t m = 0; m < nm && f * nm + m < count; m++) emit(horner_tail(pl, terms.data(), m), f * nm + m);
+    if (have) {
+      // the launch's window Horners side by side (one host thread per MSM): the last launch's are
+      // the pipeline's drain, on the critical path of the call
+      const uint32_t k = (uint32_t)std::min<size_t>(nm, count - f * nm);
+      Pt res[MSM_MAX_BATCH];
+      std::thread th[MSM_MAX_BATCH];
+      for (uint32_t m = 1; m < k; m++) th[m] = std::thread([&, m] { res[m] = horner_tail(pl, terms.data(), m); });
+      res[0] = horner_tail(pl, terms.data(), 0);
+      for (uint32_t m = 1; m < k; m++) th[m].join();
+      for (uint32_t m = 0; m < k; m++) emit(res[m], f * nm + m);
+    }
   }
   return MSM_OK;
 }
@@ -1275,8 +1290,8 @@ size_t host_piece() {
   static const size_t v = getenv("MSM_HOST_PIECE_LOG") ? (size_t)1 << atoi(getenv("MSM_HOST_PIECE_LOG")) : (size_t)1 << 17;
   return v;
 }
-uint32_t host_batch() {
-  static const uint32_t v = getenv("MSM_HOST_NM") ? (uint32_t)atoi(getenv("MSM_HOST_NM")) : 0u;
+uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices (profiles/r2kl_*)
+  static const uint32_t v = getenv("MSM_HOST_NM") ? (uint32_t)atoi(getenv("MSM_HOST_NM")) : 2u;
   return v;
 }
 
