@@ -1100,7 +1100,11 @@ int pipeline_slots(size_t n, const msm_opts* o) {
   static const int env = getenv("MSM_SLOTS") ? atoi(getenv("MSM_SLOTS")) : 0;
   if (env >= 1) return std::min(env, NSLOT);
   (void)n;
-  return 3;  // measured best at 2^16..2^20 (4 streams contend for the hardware queues)
+  // Two launches in flight.  Round 1 measured three best (one or two MSMs per launch); with two
+  // to four MSMs per launch and the one-wave-per-SIMD reduction, two beat three at every size
+  // (profiles/r2s_slots_ab.jsonl, ms per MSM, 50 steps: 2^16 0.137 vs 0.145-0.175, 2^17
+  // 0.210-0.236 vs 0.219-0.222, 2^18 0.354-0.358 vs 0.374, 2^20 1.083-1.114 vs 1.095-1.128).
+  return 2;
 }
 
 // MSMs per launch (batch) for the pipelined entries: the latency-bound kernels (reduction trees,
