@@ -75,10 +75,13 @@ const char* msm_strerror(int code);
 uint32_t msm_best_window(size_t n);
 
 /* compute_msm: host-resident inputs, result on the host.  n = 0 gives the identity (0, 1),
- * like the oracle's empty `Address.msm`.  The inputs are uploaded on a copy stream, scalars first
- * (the bucket sort starts on them) and points in 8 MiB pieces, each prepared as it lands
- * (generalises the reference's staging ring, gpu.ts:146-155 / 244-271).  The caller keeps
- * ownership of the arrays; they are not read after the call returns. */
+ * like the oracle's empty `Address.msm`.  Uploads overlap compute (generalises the reference's
+ * staging ring, gpu.ts:146-155 / 244-271): from n = 2^18 the MSM runs as point slices of >= 2^17
+ * through the pipelined launches, slice g+1 uploading on a copy stream while slice g computes,
+ * and the slices' partials are joined (the shard/join identity of submission.ts:116-154);
+ * smaller MSMs upload the scalars first (the bucket sort starts on them) and the points in 8 MiB
+ * pieces, each prepared as it lands.  The caller keeps ownership of the arrays; they are not read
+ * after the call returns. */
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                 uint32_t out_xy_be[16]);
 
