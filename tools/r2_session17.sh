@@ -19,3 +19,5 @@ done
 run bench 300 python bench.py
 run batch64 300 python bench.py --batch 64 --n 262144
 MSM_SLOTS=3 run batch64_s3 300 python bench.py --batch 64 --n 262144
+rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1 || true
+MSM_SLOTS=1 bash tools/profile_pmc.sh ${TAG}_20 > gpurun_out/${TAG}_pmc.log 2>&1 && echo "pmc ok" || echo "pmc rc=$?"

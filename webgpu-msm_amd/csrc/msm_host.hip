@@ -510,21 +510,11 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
   if (parts & PART_ACC) {
-    // MSM_ACC_WPC = k > 0: a persistent grid of k workgroups per CU strides over the tiles
-    static const uint32_t wpc = getenv("MSM_ACC_WPC") ? (uint32_t)atoi(getenv("MSM_ACC_WPC")) : 0u;
-    if (wpc && (size_t)c->n_cu * wpc < rgrid) {
-      hipLaunchKernelGGL(k_accumulate_persistent, dim3(c->n_cu * wpc), dim3(ACC_THREADS), 0, s, pts,
-                         w.sorted_entry.as<uint32_t>(), w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total,
-                         pl.K, d.W * d.B, w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(),
-                         w.lead_open.as<uint32_t>(), w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(),
-                         w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(), rgrid);
-    } else {
-      hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
-                         w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
-                         w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                         w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
-                         w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
-    }
+    hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
+                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
+                       w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
+                       w.cross_key.as<uint32_t>(), w.skew_list.as<uint32_t>(), w.g_head.as<uint32_t>(),
+                       w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>());
     mark(PH_ACCUM);
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
@@ -651,13 +641,12 @@ int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
   std::vector<hipGraphNode_t> nodes(num);
   if (hipGraphGetNodes(g, nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
   const void* f_acc = reinterpret_cast<const void*>(&k_accumulate);
-  const void* f_accp = reinterpret_cast<const void*>(&k_accumulate_persistent);
   hipGraphNode_t acc = nullptr;
   for (hipGraphNode_t nd : nodes) {
     hipGraphNodeType ty;
     hipKernelNodeParams kp{};
     if (hipGraphNodeGetType(nd, &ty) == hipSuccess && ty == hipGraphNodeTypeKernel &&
-        hipGraphKernelNodeGetParams(nd, &kp) == hipSuccess && (kp.func == f_acc || kp.func == f_accp))
+        hipGraphKernelNodeGetParams(nd, &kp) == hipSuccess && kp.func == f_acc)
       acc = nd;
   }
   if (!acc) return MSM_ERR_HIP;
@@ -1161,7 +1150,10 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm, shared);
   if (rc != MSM_OK) return rc;
-  const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)pipeline_slots(n, o)) : 1;
+  // host inputs: one more launch in flight, so its upload queues behind the running ones
+  // (2^20 msm_compute 4.21 -> 4.05 ms with three, profiles/r2t_*; device inputs are best with two)
+  const int want = pipeline_slots(n, o) + (host && !(o && (o->flags & MSM_FLAG_SERIAL)) && !getenv("MSM_SLOTS") ? 1 : 0);
+  const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)std::min(want, NSLOT)) : 1;
   for (int si = 0; si < nslot; si++) {
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
     if (host) {

@@ -899,9 +899,8 @@ __device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WOR
   }
 }
 
-// The kernel: one tile per workgroup.  k_accumulate_persistent (MSM_ACC_WPC = k) instead runs a
-// persistent grid of k workgroups per CU that strides over the tiles, leaving CU room for other
-// launches' kernels in flight beside it (a separate kernel: the loop costs registers).
+// The kernel: one tile per workgroup.  (A persistent grid of 2-3 workgroups per CU striding over
+// the tiles, to leave CU room for the other launch's kernels, measured no faster: DESIGN.md §4.1.)
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
                                          const uint32_t* __restrict__ sorted_entry,
                                          const uint32_t* __restrict__ bucket_start,
@@ -918,28 +917,8 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
                                          uint32_t* __restrict__ g_tkey) {
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
   __shared__ uint32_t sh_hkey[ACC_THREADS];
-  acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets, lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
-}
-extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate_persistent(const uint32_t* __restrict__ pts,
-                                         const uint32_t* __restrict__ sorted_entry,
-                                         const uint32_t* __restrict__ bucket_start,
-                                         const uint32_t* __restrict__ run_key,
-                                         const uint32_t* __restrict__ total_ptr, uint32_t K,
-                                         uint32_t nkeys,
-                                         uint32_t* __restrict__ buckets,
-                                         uint32_t* __restrict__ lead_val,
-                                         uint32_t* __restrict__ lead_open,
-                                         uint32_t* __restrict__ cross_key,
-                                         uint32_t* __restrict__ skew_list,
-                                         uint32_t* __restrict__ g_head,
-                                         uint32_t* __restrict__ g_hkey,
-                                         uint32_t* __restrict__ g_tkey, uint32_t ntiles) {
-  __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
-  __shared__ uint32_t sh_hkey[ACC_THREADS];
-  for (uint32_t wg = blockIdx.x; wg < ntiles; wg += gridDim.x) {
-    if (wg != blockIdx.x) __syncthreads();  // the previous tile's joins have read sh_head / sh_hkey
-    acc_tile(wg, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets, lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
-  }
+  acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets,
+           lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
 }
 
 // Joins for workgroups that k_accumulate found to hold a pass-through run (skewed scalars).
