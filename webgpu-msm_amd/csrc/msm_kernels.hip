@@ -395,9 +395,9 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
                                                                         const uint32_t* __restrict__ bin_base,
                                                                         uint32_t* __restrict__ part_entry,
                                                                         uint16_t* __restrict__ part_fine) {
-  __shared__ uint32_t st_entry[PT_THREADS * PS_R];
-  __shared__ uint16_t st_fine[PT_THREADS * PS_R];
-  __shared__ uint16_t st_bin[PT_THREADS * PS_R];
+  // one 8-B slot per staged entry: the output word (low) and fine | bin << 16 (high), so the
+  // scattered LDS write is one ds_write_b64 (three narrow ones measured heavy in bank conflicts)
+  __shared__ uint2 st[PT_THREADS * PS_R];
   extern __shared__ uint32_t dyn[];  // [nbc] local cursor, [nbc] local start, [nbc] global slice start
   uint32_t* lcur = dyn;
   uint32_t* lstart = dyn + d.nbc;
@@ -431,22 +431,18 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
       const uint32_t b = code[r] & DigitCode<T>::MAG;
       const uint32_t bin = b >> d.fb;
       const uint32_t p = atomicAdd(&lcur[bin], 1u);
-      st_entry[p] = ((pbase + i) << 1) | (code[r] >> DigitCode<T>::SHIFT);
-      st_fine[p] = (uint16_t)(b & fmask);
-      st_bin[p] = (uint16_t)bin;
+      const uint32_t ent = ((pbase + i) << 1) | (code[r] >> DigitCode<T>::SHIFT), fine = b & fmask;
+      st[p] = make_uint2(d.packed ? (ent << d.fb) | fine : ent, fine | (bin << 16));
     }
   }
   __syncthreads();
   const uint32_t m = lcur[d.nbc - 1];  // past-the-end of the last bin = live digits of the chunk
   for (uint32_t j = threadIdx.x; j < m; j += PT_THREADS) {
-    const uint32_t bin = st_bin[j];
+    const uint2 v = st[j];
+    const uint32_t bin = v.y >> 16;
     const uint32_t dst = gstart[bin] + (j - lstart[bin]);
-    if (d.packed) {
-      part_entry[dst] = (st_entry[j] << d.fb) | st_fine[j];
-    } else {
-      part_entry[dst] = st_entry[j];
-      part_fine[dst] = st_fine[j];
-    }
+    part_entry[dst] = v.x;
+    if (!d.packed) part_fine[dst] = (uint16_t)(v.y & 0xffffu);
   }
 }
 
