@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-2 GPU session 20: k_part_scatter 8-B staging vs three narrow arrays (libmsm_old.so).
+# Round-2 GPU session 20: k_fine_sort placement from the counting ranks vs a second atomic pass (libmsm_old.so).
 set -u
 mkdir -p gpurun_out
-TAG=${TAG:-r2w}
+TAG=${TAG:-r2x}
 L=$PWD/webgpu-msm_amd/msm_amd/_lib
 export TMPDIR=/tmp
 run() {
