@@ -508,7 +508,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
   }
   __syncthreads();
   const bool staged = m <= FS_CAP;
-  uint32_t fk[FS_R], en[FS_R], rk[FS_R];  // rk: the entry's rank among its bucket's (staged bins)
+  uint32_t fk[FS_R], en[FS_R];
   if (staged) {
     // every load issued before any is used; the packed/unpacked choice is uniform
     if (d.packed) {
@@ -534,7 +534,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     }
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++)
-      if (fk[r] != 0xffffu) rk[r] = atomicAdd(&cnt[fk[r]], 1u);
+      if (fk[r] != 0xffffu) atomicAdd(&cnt[fk[r]], 1u);
   } else {
     // register tiles of FS_R keys per lane (independent loads in flight); runs of equal keys
     // are collapsed before the LDS atomic
@@ -597,11 +597,13 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     }
     return;
   }
-  // the counting pass's ranks place every entry: one LDS read of its bucket's offset, no second
-  // round of atomics
 #pragma unroll
-  for (uint32_t r = 0; r < FS_R; r++)
-    if (fk[r] != 0xffffu) st_entry[cnt[fk[r]] + rk[r]] = en[r];
+  for (uint32_t r = 0; r < FS_R; r++) {
+    if (fk[r] != 0xffffu) {
+      const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
+      st_entry[p] = en[r];
+    }
+  }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
 }
