@@ -21,3 +21,5 @@ for rep in 1 2; do
   run d_16_$rep 120 $B --n 65536
   run d_17_$rep 120 $B --n 131072
 done
+run js 300 python -u -m pytest tests/test_gpu_js.py -m gpu -q --timeout 200 --timeout-method thread
+run node 300 python bench.py --no-cpu-baseline

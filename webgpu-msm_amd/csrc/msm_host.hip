@@ -1099,13 +1099,14 @@ int pipeline_slots(size_t n, const msm_opts* o) {
 // MSMs per launch (batch) for the pipelined entries: the latency-bound kernels (reduction trees,
 // scans, small sorts) of two MSMs fill the machine together.  Measured on MI355X
 // (tools/batch_sweep.sh, ms per MSM, batch 1 -> 2): 2^16 0.218 -> 0.162, 2^17 0.273 -> 0.247,
-// 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136.  Four per launch up to 2^17,
-// measured once the reduction kept one wave per SIMD (profiles/r2mn_*): 2^17 0.268 -> 0.248 ms
-// per MSM; at 2^18 within 1% of two.  MSM_BATCH overrides (1..MSM_MAX_BATCH).
+// 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136.  Four per launch up to 2^18,
+// measured once the reduction kept one wave per SIMD and two launches are in flight
+// (profiles/r2mn_*, r2y_*): 2^17 0.268 -> 0.248, 2^18 0.363 -> 0.347 ms per MSM; 2^19 +1.5%,
+// 2^20 +4.5% (kept at two).  MSM_BATCH overrides (1..MSM_MAX_BATCH).
 uint32_t pipeline_batch(size_t n, size_t count) {
   static const int env = getenv("MSM_BATCH") ? atoi(getenv("MSM_BATCH")) : 0;
   uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH)
-                         : (n <= (1u << 17) ? 4u : n <= (1u << 20) ? 2u : 1u);
+                         : (n <= (1u << 18) ? 4u : n <= (1u << 20) ? 2u : 1u);
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
