@@ -184,3 +184,22 @@ def test_serial_flag_and_profile():
     # 2^16: four MSMs per launch, so the five MSMs take two launches (the last one padded)
     assert prof["profiled"] == 2 and prof["msms_per_launch"] == 4
     assert 0 < prof["accumulate_sum"] / prof["profiled"] < 50.0
+
+
+def test_beyond_2_20_all_entries():
+    # 2^21 + 17 points: one MSM per launch in the pipelined plan, L = 8 reduction for a lone MSM,
+    # the host path as 16 slices plus a remainder; device, pipelined and host entries agree with
+    # the closed form
+    n = (1 << 21) + 17
+    pts = M.gen_points(n, k0=11, step=7)
+    scs = [M.gen_scalars(n, seed=77 + j) for j in range(3)]
+    exps = [closed_form(11, 7, s) for s in scs]
+    d_pts = _dev(pts)
+    d_sc = [_dev(s) for s in scs]
+    import torch
+
+    torch.cuda.synchronize()
+    assert M.compute_msm_device(d_pts, d_sc[0], n) == exps[0]
+    out = M.compute_msm_many_device([d_pts] * 3, d_sc, n)
+    assert [as_xy(r) for r in out] == exps
+    assert M.compute_msm_wire(pts, scs[1]) == exps[1]
