@@ -102,6 +102,10 @@ int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, s
                         uint32_t out_xyzt_be[32]);
 /* Sum `count` projective partials and return the affine result. */
 int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]);
+/* The multi-GPU join of a batch: partials [world][count][32] (as one all_gather over `world`
+ * ranks returns them); result k = sum over ranks of partial [w][k], affine, [count][16].  One
+ * field inversion for the whole batch (Montgomery's trick) instead of one per MSM. */
+int msm_combine_partials_many(const uint32_t* partials_xyzt_be, size_t world, size_t count, uint32_t* out_xy_be);
 
 /* Batch of `count` independent MSMs of equal size n, inputs contiguous ([count][n][32] points,
  * [count][n][8] scalars), all device-resident; results [count][16].  Prover-batch shape. */
@@ -109,7 +113,7 @@ int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scal
                              const msm_opts* opts, void* hip_stream, uint32_t* out_xy_be);
 
 /* `count` independent MSMs of n points each, inputs given by per-MSM device pointers; results
- * [count][16].  Pipelined: three MSMs stay on the device while the host finishes earlier ones
+ * [count][16].  Pipelined: launches of 2-4 MSMs stay on the device while the host finishes earlier ones
  * (window Horner), so throughput exceeds 1 / latency.  With window_bits = 0 the window is tuned
  * for throughput, which below 2^20 points is narrower than msm_best_window's (same results).
  * msm_compute_batch_device is this with contiguous inputs. */

@@ -104,3 +104,29 @@ def test_sharded_batch_join_gloo(world, n, k):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == [O.closed_form_msm(range(1, n + 1), O.xorshift_scalars(n, seed=1000 + b)) for b in range(k)]
+
+
+def test_batched_join_matches_per_msm_join():
+    """msm_combine_partials_many (one inversion for the batch) == msm_combine_partials per MSM,
+    on projective partials with Z != 1 (host code only, no GPU)."""
+    import msm_amd as M
+    from oracle import oracle as O
+
+    world, count = 5, 7
+    rng = np.random.default_rng(5)
+    parts = np.zeros((world, count, 32), np.uint32)
+    for w in range(world):
+        for k in range(count):
+            x, y = O.scalar_mul(O.G, int(rng.integers(1, 2**60)))
+            z = int(rng.integers(2, 2**62))
+            vals = (x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)  # (xz, yz, xyz, z)
+            parts[w, k] = np.concatenate([O.int_to_be_words(v) for v in vals])
+    got = M.combine_partials_many(parts)
+    for k in range(count):
+        assert got[k] == M.combine_partials(parts[:, k, :])
+    exp0 = O.IDENTITY
+    for w in range(world):
+        z = O.be_words_to_int(parts[w, 0, 24:32])
+        zi = O.inv(z)
+        exp0 = O.aff_add(exp0, (O.be_words_to_int(parts[w, 0, 0:8]) * zi % O.P, O.be_words_to_int(parts[w, 0, 8:16]) * zi % O.P))
+    assert got[0] == exp0

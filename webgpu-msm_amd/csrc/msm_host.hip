@@ -1535,6 +1535,36 @@ int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_
   return MSM_OK;
 }
 
+int msm_combine_partials_many(const uint32_t* partials_xyzt_be, size_t world, size_t count, uint32_t* out_xy_be) {
+  if ((!partials_xyzt_be && world && count) || (!out_xy_be && count)) return MSM_ERR_INVALID_ARG;
+  std::vector<Pt> acc(count, pt_identity());
+  for (size_t k = 0; k < count; k++)
+    for (size_t w = 0; w < world; w++) {
+      Pt p;
+      int rc = pt_from_be_xyzt(partials_xyzt_be + 32 * (w * count + k), &p);
+      if (rc != MSM_OK) return rc;
+      if (fq_is_zero(p.Z)) return MSM_ERR_BAD_POINT;
+      acc[k] = w == 0 ? p : pt_add(acc[k], p);
+    }
+  if (!count) return MSM_OK;
+  // Montgomery's trick: one inversion of the product of every Z, then each Z^-1 from prefix
+  // products (complete formulas: a sum of valid points never has Z = 0)
+  std::vector<Fq> pre(count);
+  pre[0] = acc[0].Z;
+  for (size_t k = 1; k < count; k++) pre[k] = fq_mul(pre[k - 1], acc[k].Z);
+  Fq inv = fq_inv(pre[count - 1]);
+  for (size_t k = count; k-- > 0;) {
+    const Fq zi = k ? fq_mul(inv, pre[k - 1]) : inv;
+    if (k) inv = fq_mul(inv, acc[k].Z);
+    uint64_t x[4], y[4];
+    fq_to_std(fq_mul(acc[k].X, zi), x);
+    fq_to_std(fq_mul(acc[k].Y, zi), y);
+    std_to_be_words(x, out_xy_be + 16 * k);
+    std_to_be_words(y, out_xy_be + 16 * k + 8);
+  }
+  return MSM_OK;
+}
+
 int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16], uint32_t out_xy_be[16]) {
   if (!a_xy_be || !b_xy_be || !out_xy_be) return MSM_ERR_INVALID_ARG;
   uint64_t ax[4], ay[4], bx[4], by[4];

@@ -22,7 +22,7 @@ __all__ = [
     "MsmError", "MsmOpts", "load", "compute_msm", "compute_msm_wire", "compute_msm_device",
     "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "compute_msm_many_device_partial",
     "compute_msm_shared_device", "compute_msm_many", "compute_msm_shared", "compute_msm_cpu", "MSM_FLAG_SERIAL",
-    "combine_partials", "point_add_affine",
+    "combine_partials", "combine_partials_many", "point_add_affine",
     "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
@@ -104,6 +104,7 @@ def load() -> ctypes.CDLL:
         "msm_compute_shared": ([vp, vp, sz, sz, optp, u32p], ctypes.c_int),
         "msm_compute_cpu": ([vp, vp, sz, ctypes.c_uint32, ctypes.c_int, u32p], ctypes.c_int),
         "msm_combine_partials": ([vp, sz, u32p], ctypes.c_int),
+        "msm_combine_partials_many": ([vp, sz, sz, u32p], ctypes.c_int),
         "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
         "msm_split": ([ctypes.c_uint32, vp, sz, u32p], ctypes.c_int),
         "msm_split_windows": ([ctypes.c_uint32], ctypes.c_uint32),
@@ -415,6 +416,16 @@ def combine_partials(partials: np.ndarray) -> Tuple[int, int]:
     o, op = _out(16)
     _check(L.msm_combine_partials(_ptr(p), p.shape[0], op), "msm_combine_partials")
     return _xy(o)
+
+
+def combine_partials_many(parts: np.ndarray):
+    """parts [world, K, 32] (an all_gather of K partials per rank) -> the K joined affine results."""
+    L = load()
+    p = np.ascontiguousarray(_u32(parts))
+    world, count = p.shape[0], p.shape[1]
+    o, op = _out(16 * max(count, 1))
+    _check(L.msm_combine_partials_many(_ptr(p.reshape(-1)), world, count, op), "msm_combine_partials_many")
+    return [_xy(o[16 * k: 16 * k + 16]) for k in range(count)]
 
 
 def point_add_affine(a: Tuple[int, int], b: Tuple[int, int]) -> Tuple[int, int]:

@@ -35,12 +35,13 @@ def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.
 
 
 def combine_batch_on_root(parts: np.ndarray, rank: int, root: int = 0):
-    """parts [world, K, 32]: rank `root` joins each of the K MSMs' world partials."""
+    """parts [world, K, 32]: rank `root` joins each of the K MSMs' world partials in one libmsm
+    call (one field inversion for the batch)."""
     if rank != root:
         return None
-    from . import combine_partials
+    from . import combine_partials_many
 
-    return [combine_partials(parts[:, k, :]) for k in range(parts.shape[1])]
+    return combine_partials_many(parts)
 
 
 def combine_on_root(parts: np.ndarray, rank: int, root: int = 0) -> Optional[Tuple[int, int]]:
