@@ -299,10 +299,11 @@ uint32_t ilog2(uint32_t v) {
 
 // Window width for MSMs kept in flight by the pipelined entries (whole-job throughput rather
 // than one MSM's latency): there the bucket reduction's work, not its latency, is what counts,
-// so sub-2^20 sizes prefer narrower windows.  Measured on MI355X (tools/window_sweep.sh): c = 14
-// at 2^16, 15 at 2^17..2^19 (-16% at 2^17 vs c = 16), 16 from 2^20.
+// so sub-2^20 sizes prefer narrower windows.  Measured on MI355X (tools/window_sweep.sh; round 2
+// re-check with the current launch plan, profiles/r2ab_window_ab.jsonl): c = 14 at 2^16, 15 at
+// 2^17..2^18, 16 from 2^19 (2^19: 0.584-0.592 vs 0.604-0.614 ms at c = 15).
 uint32_t pipelined_window(size_t n) {
-  if (n >= (1u << 20)) return 16;
+  if (n >= (1u << 19)) return 16;
   if (n >= (1u << 17)) return 15;
   if (n >= (1u << 15)) return 14;
   return msm_best_window(n);
