@@ -333,6 +333,22 @@ uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
   return 16;
 }
 
+// Run length K (entries per k_accumulate lane, a multiple of 4 for the 16-B entry loads): the
+// accumulation holds 4 waves per SIMD (VGPR- and LDS-bound), so its lanes run in rounds of
+// 4 x 4 x CUs waves, and a round only partly filled runs on few SIMDs for a full wave's time.
+// So K <= 64 (long enough to amortise the per-run joins) is chosen to fill whole rounds: the
+// fewest rounds r with K <= 64, then the smallest K that fits the launch's entries in r rounds
+// (upper bound: every main-window digit nonzero).  2^20, two MSMs: K = 64, 2 rounds; 2^17, four
+// MSMs: K = 36 (3,868 waves) where K = 32 needed 4,352, a 6% second round.
+uint32_t run_length_for(const MsmDims& d, int n_cu) {
+  const uint64_t m = (uint64_t)d.nm * (d.Wm - 1) * d.n;
+  const uint64_t round_lanes = 64ull * 4 * 4 * (uint64_t)(n_cu > 0 ? n_cu : 256);
+  const uint64_t r = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
+  uint64_t K = (m + r * round_lanes - 1) / (r * round_lanes);
+  K = (K + 3) & ~3ull;
+  return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, K));
+}
+
 int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1,
               bool shared = false) {
   *pl = Plan{};
@@ -365,11 +381,7 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
   pl->d = d;
-  // Run length: long enough to amortise the per-run head/tail joins, short enough to leave
-  // ~4 waves per SIMD (262144 lanes) of accumulation work.
-  uint32_t kauto = 64;
-  while (kauto > 16 && (size_t)d.W * n / kauto < 262144) kauto >>= 1;
-  pl->K = (o && o->run_length) ? o->run_length : kauto;
+  pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, n_cu);
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
   pl->L = bucket_reduce_L(d, n_cu);
   pl->nchunks = (d.B + pl->L - 1) / pl->L;
