@@ -1,5 +1,6 @@
 """The TypeScript/JS drop-in (webgpu-msm_amd/js/submission.mjs) end to end on the GPU:
-compute_msm with BigIntPoint[]/bigint[] and U32ArrayPoint[]/Uint32Array[] inputs."""
+compute_msm with BigIntPoint[]/bigint[] and U32ArrayPoint[]/Uint32Array[] inputs, and with
+flat wire buffers (the marshalling-free extension)."""
 import json
 import os
 import shutil
@@ -16,7 +17,7 @@ NODE = shutil.which("node")
 
 
 @pytest.mark.skipif(NODE is None, reason="node not installed")
-@pytest.mark.parametrize("form", ["bigint", "u32"])
+@pytest.mark.parametrize("form", ["bigint", "u32", "flat"])
 def test_compute_msm_js(form, tmp_path):
     n = 500
     pts = O.gen_points(n, k0=21, step=13)
@@ -33,9 +34,14 @@ let points, scalars;
 if ("{form}" === "bigint") {{
   points = d.pts.map(([x, y, t, z]) => ({{x: BigInt(x), y: BigInt(y), t: BigInt(t), z: BigInt(z)}}));
   scalars = d.sc.map(BigInt);
-}} else {{
+}} else if ("{form}" === "u32") {{
   points = d.pts.map(([x, y, t, z]) => ({{x: toWords(x), y: toWords(y), t: toWords(t), z: toWords(z)}}));
   scalars = d.sc.map(toWords);
+}} else {{  // flat wire buffers (the extension): n x 32 and n x 8 words
+  points = new Uint32Array(d.pts.length * 32);
+  d.pts.forEach((r, i) => r.forEach((v, j) => points.set(toWords(v), 32 * i + 8 * j)));
+  scalars = new Uint32Array(d.sc.length * 8);
+  d.sc.forEach((v, i) => scalars.set(toWords(v), 8 * i));
 }}
 m.compute_msm(points, scalars).then((r) => console.log(r.x.toString() + "," + r.y.toString()),
   (e) => {{ console.error(e); process.exit(3); }});

@@ -46,9 +46,18 @@ const expect = xArg ? { x: BigInt(xArg), y: BigInt(yArg) } : null;
     flattenU32(points, scalars);
     flat.push(performance.now() - t0);
   }
+  // the same MSM from flat wire buffers (no marshalling): the addon + libmsm share
+  const flatTimes = [];
+  for (let r = 0; r <= runs; r++) {
+    const t0 = performance.now();
+    const res = await compute_msm(pw, sw);
+    const t1 = performance.now();
+    if (r > 0) flatTimes.push(t1 - t0);
+    if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
+  }
   const med = (xs) => [...xs].sort((a, b) => a - b)[Math.floor(xs.length / 2)];
-  console.log(JSON.stringify({ node_e2e_ms: med(times), marshal_ms: med(flat), runs_ms: times,
-                               correct: expect ? ok : null }));
+  console.log(JSON.stringify({ node_e2e_ms: med(times), marshal_ms: med(flat), flat_input_ms: med(flatTimes),
+                               runs_ms: times, correct: expect ? ok : null }));
 })().catch((e) => {
   console.log(JSON.stringify({ error: String(e) }));
   process.exit(1);

@@ -5,6 +5,9 @@
 //   compute_msm(baseAffinePoints: BigIntPoint[] | U32ArrayPoint[],
 //               scalars: bigint[] | Uint32Array[]) => Promise<{ x: bigint, y: bigint }>
 //
+// Also accepted (an extension): flat wire buffers, a Uint32Array of n x 32 point words and one of
+// n x 8 scalar words -- the layout flattenU32 builds -- which skips the JS marshalling.
+//
 // The browser-only knobs (?windowSize=, submission.ts:29-33) become an optional third
 // argument { windowSize } or the MSM_WINDOW_SIZE environment variable.  { cpuWorkRatio }
 // (?cpuWorkRatio, submission.ts:96-154) is accepted and the whole MSM runs on the GPU: the host
@@ -70,6 +73,14 @@ export function flattenU32(points, scalars) {
 
 export const compute_msm = async (baseAffinePoints, scalars, options) => {
   const windowSize = windowFrom(options);
+  if (baseAffinePoints instanceof Uint32Array && scalars instanceof Uint32Array) {
+    // already flat wire buffers (x|y|t|z BE words per point, BE words per scalar): no marshalling
+    const n = Math.min(Math.floor(baseAffinePoints.length / nUint32PerPoint), Math.floor(scalars.length / nUint32PerScalar));
+    const result = await addon.computeMsmU32(baseAffinePoints.subarray(0, n * nUint32PerPoint),
+                                             scalars.subarray(0, n * nUint32PerScalar), windowSize);
+    const [x, y] = u32ArrayToBigInts(result);
+    return { x, y };
+  }
   const hasBigInt =
     (baseAffinePoints.length > 0 && typeof baseAffinePoints[0].x === "bigint") ||
     (scalars.length > 0 && typeof scalars[0] === "bigint");
