@@ -453,13 +453,22 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
 
 inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
+// Whether k_prepare_points writes `records` point records with nontemporal stores: only when they
+// outgrow the Infinity Cache (>= 128 MiB, i.e. 2^20 records; MSM_PP_NT=0/1 forces it).
+uint32_t prep_nt(size_t records) {
+  static const int forced = getenv("MSM_PP_NT") ? atoi(getenv("MSM_PP_NT")) : -1;
+  if (forced >= 0) return forced ? 1u : 0u;
+  return records * 128 >= (size_t(1) << 27) ? 1u : 0u;
+}
+
 // k_prepare_points over `cnt` points of one wire buffer into `pts_out` (one MSM, or one uploaded
-// chunk of it).
-void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint32_t* err, hipStream_t s) {
+// chunk of it); `nt` from prep_nt of the whole record buffer.
+void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint32_t* err, uint32_t nt,
+                    hipStream_t s) {
   BatchPtrs bp{};
   bp.p[0] = wire;
   hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(cnt, PP_THREADS), 1), dim3(PP_THREADS), 0, s, bp, pts_out, cnt,
-                     err);
+                     err, nt);
 }
 
 // Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
@@ -480,7 +489,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   if (parts & PART_PREP) {
     mark(PH_START);
     hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, s,
-                       d_points, pts, d.n, w.err.as<uint32_t>());
+                       d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n));
     mark(PH_PREPARE);
   }
   if (parts & PART_SORT) {
@@ -750,7 +759,8 @@ int repoint_inputs(const Plan& pl, Slot& sl, Segment& sg, const BatchPtrs& d_poi
     uint32_t* ptsb = const_cast<uint32_t*>(sg.pts_buf);
     uint32_t n = d.n;
     uint32_t* err = w.err.as<uint32_t>();
-    void* a_prep[] = {&wire, &ptsb, &n, &err};
+    uint32_t nt = prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n);
+    void* a_prep[] = {&wire, &ptsb, &n, &err, &nt};
     hipKernelNodeParams kp = sg.p_prep;
     kp.kernelParams = a_prep;
     kp.extra = nullptr;
@@ -1026,7 +1036,7 @@ int upload_points(DevCtx* c, const uint32_t* points_be, size_t n, uint32_t* wire
     HIPCHECK(hipEventRecord(e, c->copy_stream));
     HIPCHECK(hipStreamWaitEvent(s, e, 0));
     const size_t p0 = off / 128;
-    launch_prepare(wire + p0 * 32, pts + p0 * PRE_WORDS, (uint32_t)(b / 128), err, s);
+    launch_prepare(wire + p0 * 32, pts + p0 * PRE_WORDS, (uint32_t)(b / 128), err, prep_nt(n), s);
     HIPCHECK(hipGetLastError());
     return MSM_OK;
   });
@@ -1195,7 +1205,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
                          s0.stream);
       if (rc != MSM_OK) return fail(rc);
     } else {
-      launch_prepare(in.shared_points, pts_shared, (uint32_t)n, s0.ws.err.as<uint32_t>(), s0.stream);
+      launch_prepare(in.shared_points, pts_shared, (uint32_t)n, s0.ws.err.as<uint32_t>(), prep_nt(n), s0.stream);
       if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
     }
     if (hipEventRecord(c->ev_shared, s0.stream) != hipSuccess) return fail(MSM_ERR_HIP);
