@@ -1230,20 +1230,27 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         bp.p[m] = shared ? in.shared_points : in.points[b];
         bs.p[m] = in.scalars[b];
         if (host && m < nm) {
-          // this slot's previous launch has finished (above): its wire buffers are free
-          uint32_t* wsc = sl.ws.wire_sc.as<uint32_t>() + (size_t)m * n * 8;
-          if (hipMemcpyAsync(wsc, in.scalars[b], n * 32, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
-            return fail(MSM_ERR_HIP);
-          bs.p[m] = wsc;
-          if (!shared) {
-            uint32_t* wp = sl.ws.wire_pts.as<uint32_t>() + (size_t)m * n * 32;
-            if (hipMemcpyAsync(wp, in.points[b], n * 128, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
-              return fail(MSM_ERR_HIP);
-            bp.p[m] = wp;
-          }
+          bs.p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)m * n * 8;
+          if (!shared) bp.p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)m * n * 32;
         }
       }
       if (host) {
+        // this slot's previous launch has finished (above): its wire buffers are free.  MSMs whose
+        // host arrays are adjacent (the slices of run_host_split) go up in one copy per array:
+        // each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between transfers.
+        auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t words) -> bool {
+          for (uint32_t m0 = 0; m0 < nm;) {
+            const uint32_t* h0 = src[std::min(j * nm + m0, count - 1)];
+            uint32_t m1 = m0 + 1;
+            while (m1 < nm && j * nm + m1 < count && src[j * nm + m1] == h0 + (size_t)(m1 - m0) * words) m1++;
+            if (hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, (size_t)(m1 - m0) * words * 4,
+                               hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+              return false;
+            m0 = m1;
+          }
+          return true;
+        };
+        if (!up(in.scalars, bs, n * 8) || (!shared && !up(in.points, bp, n * 32))) return fail(MSM_ERR_HIP);
         for (uint32_t m = nm; m < MSM_MAX_BATCH; m++) {
           bp.p[m] = bp.p[nm - 1];
           bs.p[m] = bs.p[nm - 1];
