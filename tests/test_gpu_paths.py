@@ -47,6 +47,29 @@ def test_host_entry_split_into_slices(n):
     assert M.combine_partials(np.asarray(part, dtype=np.uint32).reshape(1, 32)) == exp
 
 
+def test_host_split_projective_points():
+    # the split host path with projective points (z != 1, normalised by k_prepare_points) in one
+    # launch's slices and in the remainder MSM; z = 0 in another launch is still rejected
+    from oracle import oracle as O
+
+    n = (1 << 19) + 5  # four slices in two launches, and a one-point remainder
+    pts = M.gen_points(n, k0=9, step=7)
+    sc = M.gen_scalars(n, seed=77)
+    exp = closed_form(9, 7, sc)
+    # projective points in launch 0 (slices 0 and 1) and in the remainder
+    for i, z in ((3, 2), ((1 << 17) + 11, 12345678901), (n - 1, O.P - 2)):
+        x, y, t = (O.be_words_to_int(pts[i, 8 * j: 8 * j + 8]) for j in range(3))
+        for j, v in enumerate((x * z % O.P, y * z % O.P, t * z % O.P, z)):
+            pts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
+    assert M.compute_msm_wire(pts, sc) == exp
+    pts[(1 << 18) + 20, 24:32] = 0  # launch 1
+    with pytest.raises(M.MsmError) as e:
+        M.compute_msm_wire(pts, sc)
+    assert e.value.code == -4
+    # affine again: the same result
+    assert M.compute_msm_wire(M.gen_points(n, k0=9, step=7), sc) == exp
+
+
 def test_host_many_distinct():
     cases = []
     for j, n in enumerate((3000, 3000, 3000, 3000, 3000)):

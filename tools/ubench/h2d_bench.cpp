@@ -133,6 +133,26 @@ int main(int argc, char** argv) {
     snprintf(ex, sizeof ex, ", \"register_ms\": %.3f, \"copy_ms\": %.3f, \"unregister_ms\": %.3f", reg, cp, unreg);
     if (r == 1) rep("host_register_copy", reg + cp + unreg, ex);
   }
+  // register a FRESH buffer each time (first-touch pages, never registered before): the cost a
+  // caller's new arrays would pay
+  for (int r = 0; r < 3; r++) {
+    char* fresh = (char*)aligned_alloc(4096, total);
+    memcpy(fresh, host, total);
+    auto t0 = clk::now();
+    CK(hipHostRegister(fresh, total, hipHostRegisterDefault));
+    double reg = ms_since(t0);
+    auto t1 = clk::now();
+    CK(hipMemcpyAsync(dev, fresh, total, hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    double cp = ms_since(t1);
+    auto t2 = clk::now();
+    CK(hipHostUnregister(fresh));
+    double unreg = ms_since(t2);
+    char ex[128];
+    snprintf(ex, sizeof ex, ", \"register_ms\": %.3f, \"copy_ms\": %.3f, \"unregister_ms\": %.3f", reg, cp, unreg);
+    rep("fresh_register_copy", reg + cp + unreg, ex);
+    free(fresh);
+  }
   // host memcpy pageable -> pinned, T threads
   for (int th : {1, 4, 8, 16, 32}) {
     Pool pool(th);
