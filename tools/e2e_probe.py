@@ -34,8 +34,7 @@ def main():
         r = M.compute_msm_wire(pts, sc)
         times.append(round((time.perf_counter() - t0) * 1e3, 3))
         ok.append(exp is None or r == exp)
-    print(json.dumps({"n": args.n, "e2e_ms": times, "correct": all(ok),
-                      "pin": os.environ.get("MSM_H2D_PIN", "0")}))
+    print(json.dumps({"n": args.n, "e2e_ms": times, "correct": all(ok)}))
 
 
 if __name__ == "__main__":

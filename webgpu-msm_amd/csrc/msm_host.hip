@@ -1051,29 +1051,6 @@ int upload_scalars(DevCtx* c, const uint32_t* scalars_be, size_t n, uint32_t* wi
   return MSM_OK;
 }
 
-// The caller's host array, pinned in place for the call when MSM_H2D_PIN=1 (hipHostRegister:
-// the pieces' copies then DMA straight from it, asynchronously).  Pinned memory is used as is.
-struct HostPin {
-  DevCtx* c = nullptr;
-  void* p = nullptr;
-  bool reg = false;
-  HostPin(DevCtx* ctx, const void* ptr, size_t bytes) : c(ctx) {
-    static const bool on = getenv("MSM_H2D_PIN") && atoi(getenv("MSM_H2D_PIN")) == 1;
-    if (!on || !bytes) return;
-    if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess) {
-      p = const_cast<void*>(ptr);
-      reg = true;
-    } else {
-      (void)hipGetLastError();  // already pinned, or not registrable: plain copies
-    }
-  }
-  ~HostPin() {
-    if (!reg) return;
-    hipStreamSynchronize(c->copy_stream);  // no copy may still read it
-    hipHostUnregister(p);
-  }
-};
-
 // One MSM of host-resident inputs: the scalars go up first and the bucket sort starts on them
 // while the points upload piece by piece, each piece prepared as it lands; accumulation starts
 // after the last piece.  The end-to-end time is then ~ PCIe transfer + the post-upload tail.
@@ -1094,7 +1071,6 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   sl.pl = pl;
   uint32_t* pts = w.pts.as<uint32_t>();
   const BatchPtrs bp = splat(w.wire_pts.as<uint32_t>()), bs = splat(w.wire_sc.as<uint32_t>());
-  HostPin pin_sc(c, scalars_be, n * 32), pin_pts(c, points_be, n * 128);
   if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK) return rc;
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return rc;
   if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
