@@ -4,7 +4,7 @@ issue cycles it demands per wave-iteration on gfx950.
     python tools/isa_mix.py [--out profiles/r2_isa_mix.json]
 
 Compiles libmsm's device code with --save-temps into a scratch directory, takes the basic block
-of k_accumulate holding the most v_mad_u64_u32 (one pt_madd per wave-iteration), and prices it
+of k_accumulate holding the most 64-bit multiply-adds (one pt_madd per wave-iteration), and prices it
 two ways:
   * cycles_per_iteration: the nominal gfx950 model (a SIMD-32 issues a 32-bit VALU wave64
     instruction in 2 cycles, a 64-bit one -- v_mad_u64_u32, 64-bit shifts/adds/moves -- in 4);
@@ -24,6 +24,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "webgpu-msm_amd", "csrc", "msm_host.hip")
+MADS = ("v_mad_u64_u32", "v_mad_i64_i32")
 VALU64 = {"v_mad_u64_u32", "v_mad_i64_i32", "v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_mov_b64",
           "v_add_u64", "v_ashrrev_i64", "v_fma_f64"}
 
@@ -101,13 +102,13 @@ def main():
         blocks, loops = blocks_of(asm_text(tmp), args.func)
     # the loop block with the most multiplies: one entry's pt_madd per wave-iteration
     name, ins = max(((k, v) for k, v in blocks.items() if k in loops),
-                    key=lambda kv: sum(1 for o in kv[1] if o == "v_mad_u64_u32"))
+                    key=lambda kv: sum(1 for o in kv[1] if o in MADS))
     cnt = collections.Counter(base(o) for o in ins)
     v64 = sum(c for o, c in cnt.items() if o in VALU64)
     v32 = sum(c for o, c in cnt.items() if o.startswith("v_") and o not in VALU64)
     cycles = 4 * v64 + 2 * v32
     res = {"kernel": args.func, "block": name, "instructions": len(ins), "valu64": v64, "valu32": v32,
-           "v_mad_u64_u32": cnt["v_mad_u64_u32"],
+           "v_mad_u64_u32": cnt["v_mad_u64_u32"], "v_mad_i64_i32": cnt["v_mad_i64_i32"],
            "vmem_loads": sum(c for o, c in cnt.items() if o.startswith(("global_load", "buffer_load"))),
            "cycles_per_iteration": cycles,
            "cycle_model": "gfx950 SIMD-32: 2 cycles per 32-bit VALU wave64 instruction, 4 per 64-bit one "
