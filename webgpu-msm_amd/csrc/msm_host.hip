@@ -1109,6 +1109,13 @@ uint32_t pipeline_batch(size_t n, size_t count) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
+// Whether a host-input pipelined run starts its last launch's sort before that launch's points
+// upload (MSM_HOST_SORT_EARLY=0 disables, for A/B runs).
+bool host_sort_early() {
+  static const bool on = !(getenv("MSM_HOST_SORT_EARLY") && atoi(getenv("MSM_HOST_SORT_EARLY")) == 0);
+  return on;
+}
+
 // Where the inputs of one pipelined run come from.
 struct ManyInputs {
   enum Kind { DEVICE, HOST } kind = DEVICE;
@@ -1210,6 +1217,9 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
           if (!shared) bp.p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)m * n * 32;
         }
       }
+      const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
+      uint32_t* pts = shared ? pts_shared : sl.ws.pts.as<uint32_t>();
+      const bool sort_early = host && !shared && j + 1 == nbatch && nbatch > 1 && host_sort_early();
       if (host) {
         // this slot's previous launch has finished (above): its wire buffers are free.  MSMs whose
         // host arrays are adjacent (the slices of run_host_split) go up in one copy per array:
@@ -1226,18 +1236,28 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
           }
           return true;
         };
-        if (!up(in.scalars, bs, n * 8) || (!shared && !up(in.points, bp, n * 32))) return fail(MSM_ERR_HIP);
         for (uint32_t m = nm; m < MSM_MAX_BATCH; m++) {
           bp.p[m] = bp.p[nm - 1];
           bs.p[m] = bs.p[nm - 1];
         }
+        if (!up(in.scalars, bs, n * 8)) return fail(MSM_ERR_HIP);
+        // The last launch's bucket sort starts on its scalars while its points upload: the sort
+        // then leaves the call's tail (earlier launches overlap the next uploads anyway, and an
+        // extra graph launch between their copies would only widen the copy engine's gaps).
+        if (sort_early) {
+          if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
+              hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
+            return fail(MSM_ERR_HIP);
+          sl.pl = pl;
+          if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
+        }
+        if (!shared && !up(in.points, bp, n * 32)) return fail(MSM_ERR_HIP);
         if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
             hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
           return fail(MSM_ERR_HIP);
       }
       sl.pl = pl;
-      const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
-      if ((rc = launch_parts(c, pl, bp, bs, si, parts, shared ? pts_shared : sl.ws.pts.as<uint32_t>())) != MSM_OK)
+      if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
         return fail(rc);
     }
     if (have) {
