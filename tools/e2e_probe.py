@@ -34,7 +34,8 @@ def main():
         r = M.compute_msm_wire(pts, sc)
         times.append(round((time.perf_counter() - t0) * 1e3, 3))
         ok.append(exp is None or r == exp)
-    print(json.dumps({"n": args.n, "e2e_ms": times, "correct": all(ok)}))
+    print(json.dumps({"n": args.n, "e2e_ms": times, "correct": all(ok) if exp else None,
+                      "x_low64": hex(r[0] & (2**64 - 1))}))
 
 
 if __name__ == "__main__":

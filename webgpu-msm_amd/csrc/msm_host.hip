@@ -1123,6 +1123,8 @@ struct ManyInputs {
   const uint32_t* const* scalars = nullptr;
   const uint32_t* shared_points = nullptr;  // one base vector for every MSM (prover batch)
   uint32_t batch = 0;                        // MSMs per launch (0: pipeline_batch's choice)
+  const size_t* lens = nullptr;  // host inputs: real points per MSM (<= n; the rest is padded on
+                                 // the device with identity points and zero scalars); null: all n
 };
 
 // `count` MSMs of n points each, pipelined over pipeline_slots slots, each with its own stream and
@@ -1224,13 +1226,20 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         // this slot's previous launch has finished (above): its wire buffers are free.  MSMs whose
         // host arrays are adjacent (the slices of run_host_split) go up in one copy per array:
         // each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between transfers.
-        auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t words) -> bool {
+        // A short MSM (in.lens) goes up alone and its tail is padded on the device.
+        auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
+        auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
           for (uint32_t m0 = 0; m0 < nm;) {
-            const uint32_t* h0 = src[std::min(j * nm + m0, count - 1)];
+            const size_t b0 = std::min(j * nm + m0, count - 1);
+            const uint32_t* h0 = src[b0];
             uint32_t m1 = m0 + 1;
-            while (m1 < nm && j * nm + m1 < count && src[j * nm + m1] == h0 + (size_t)(m1 - m0) * words) m1++;
-            if (hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, (size_t)(m1 - m0) * words * 4,
-                               hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+            if (len_of(b0) == n)
+              while (m1 < nm && j * nm + m1 < count && len_of(j * nm + m1) == n &&
+                     src[j * nm + m1] == h0 + (size_t)(m1 - m0) * n * per)
+                m1++;
+            const size_t words = (m1 - m0 == 1 ? len_of(b0) : (size_t)(m1 - m0) * n) * per;
+            if (words && hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, words * 4, hipMemcpyHostToDevice,
+                                        c->copy_stream) != hipSuccess)
               return false;
             m0 = m1;
           }
@@ -1240,7 +1249,16 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
           bp.p[m] = bp.p[nm - 1];
           bs.p[m] = bs.p[nm - 1];
         }
-        if (!up(in.scalars, bs, n * 8)) return fail(MSM_ERR_HIP);
+        if (!up(in.scalars, bs, 8)) return fail(MSM_ERR_HIP);
+        for (uint32_t m = 0; m < nm && !shared; m++) {
+          const size_t len = len_of(std::min(j * nm + m, count - 1));
+          if (len < n) {
+            hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
+                               const_cast<uint32_t*>(bp.p[m]) + len * 32, const_cast<uint32_t*>(bs.p[m]) + len * 8,
+                               (uint32_t)(n - len));
+            if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
+          }
+        }
         // The last launch's bucket sort starts on its scalars while its points upload: the sort
         // then leaves the call's tail (earlier launches overlap the next uploads anyway, and an
         // extra graph launch between their copies would only widen the copy engine's gaps).
@@ -1251,7 +1269,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
           sl.pl = pl;
           if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
         }
-        if (!shared && !up(in.points, bp, n * 32)) return fail(MSM_ERR_HIP);
+        if (!shared && !up(in.points, bp, 32)) return fail(MSM_ERR_HIP);
         if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
             hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
           return fail(MSM_ERR_HIP);
@@ -1322,29 +1340,31 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
 // MSM = sum_g MSM(slice g), the reference's own shard/join identity (submission.ts:116-154,
 // lib.rs:240-253) inside one GPU.  The slices go through the pipelined entry: slice g+1 uploads
 // on the copy stream while slice g runs, so the PCIe transfer -- the bulk of a host-input MSM --
-// overlaps all the compute but the last launch's; the partials are joined with G - 1 adds.  A
-// remainder of fewer than G points (n not a multiple of G) is one more small MSM.
+// overlaps all the compute but the last launch's; the partials are joined with G - 1 adds.  When
+// G does not divide n the last slice is short: it is padded on the device (identity points, zero
+// scalars) rather than run as a separate remainder MSM after the others.
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
   const size_t G = std::min<size_t>(16, n / host_piece());
-  const size_t s = n / G, done = G * s;
+  const size_t s = (n + G - 1) / G;  // (G - 1) s < n for G <= 16 <= sqrt(n): every slice is non-empty
   std::vector<const uint32_t*> pp(G), ss(G);
+  std::vector<size_t> lens(G);
   for (size_t g = 0; g < G; g++) {
     pp[g] = points_be + g * s * 32;
     ss[g] = scalars_be + g * s * 8;
+    lens[g] = std::min(s, n - g * s);
   }
   ManyInputs in;
   in.kind = ManyInputs::HOST;
   in.points = pp.data();
   in.scalars = ss.data();
   in.batch = host_batch();
-  std::vector<Pt> part(G + 1, pt_identity());
+  in.lens = lens.data();
+  std::vector<Pt> part(G, pt_identity());
   int rc = run_many(c, in, s, G, o, nullptr, nullptr, true, part.data());
   if (rc != MSM_OK) return rc;
-  if (done < n && (rc = run_host(c, points_be + done * 32, scalars_be + done * 8, n - done, o, &part[G])) != MSM_OK)
-    return rc;
   Pt acc = part[0];
-  for (size_t g = 1; g <= G; g++) acc = pt_add(acc, part[g]);
+  for (size_t g = 1; g < G; g++) acc = pt_add(acc, part[g]);
   *result = acc;
   return MSM_OK;
 }

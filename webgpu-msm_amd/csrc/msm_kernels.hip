@@ -158,6 +158,20 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
   }
 }
 
+// Pads a short host-input slice on the device (run_host_split with n not a multiple of its slice
+// count): `count` wire points set to the identity (x, y, t, z) = (0, 1, 0, 1) and `count` scalars
+// set to 0, so the padding contributes no bucket entry.  16-B stores, one per thread.
+extern "C" __global__ void __launch_bounds__(256) k_pad_identity(uint32_t* __restrict__ wire_pts,
+                                                                   uint32_t* __restrict__ wire_sc, uint32_t count) {
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;  // 16-B slot: 8 per point, then 2 per scalar
+  if (g < count * 8) {
+    const uint32_t q = g & 7;  // BE words: the least significant word of y (slot 3) and z (slot 7)
+    reinterpret_cast<uint4*>(wire_pts)[g] = make_uint4(0u, 0u, 0u, (q == 3 || q == 7) ? 1u : 0u);
+  } else if (g < count * 10) {
+    reinterpret_cast<uint4*>(wire_sc)[g - count * 8] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 __device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32_t idx) {
   const uint4* src = reinterpret_cast<const uint4*>(pts + (size_t)idx * 32);
   uint32_t rec[28];
