@@ -1210,13 +1210,15 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       const int si = (int)(j % nslot);
       Slot& sl = c->slot[si];
       BatchPtrs bp{}, bs{};
+      const uint32_t nreal = (uint32_t)std::min<size_t>(nm, count - j * nm);  // MSMs of this launch
       for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
         const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
         bp.p[m] = shared ? in.shared_points : in.points[b];
         bs.p[m] = in.scalars[b];
-        if (host && m < nm) {
-          bs.p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)m * n * 8;
-          if (!shared) bp.p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)m * n * 32;
+        if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
+          const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
+          bs.p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
+          if (!shared) bp.p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
         }
       }
       const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
@@ -1226,15 +1228,16 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         // this slot's previous launch has finished (above): its wire buffers are free.  MSMs whose
         // host arrays are adjacent (the slices of run_host_split) go up in one copy per array:
         // each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between transfers.
+        // The padding MSMs of a short last launch upload nothing.
         // A short MSM (in.lens) goes up alone and its tail is padded on the device.
         auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
         auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
-          for (uint32_t m0 = 0; m0 < nm;) {
+          for (uint32_t m0 = 0; m0 < nreal;) {
             const size_t b0 = std::min(j * nm + m0, count - 1);
             const uint32_t* h0 = src[b0];
             uint32_t m1 = m0 + 1;
             if (len_of(b0) == n)
-              while (m1 < nm && j * nm + m1 < count && len_of(j * nm + m1) == n &&
+              while (m1 < nreal && len_of(j * nm + m1) == n &&
                      src[j * nm + m1] == h0 + (size_t)(m1 - m0) * n * per)
                 m1++;
             const size_t words = (m1 - m0 == 1 ? len_of(b0) : (size_t)(m1 - m0) * n) * per;
@@ -1245,12 +1248,8 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
           }
           return true;
         };
-        for (uint32_t m = nm; m < MSM_MAX_BATCH; m++) {
-          bp.p[m] = bp.p[nm - 1];
-          bs.p[m] = bs.p[nm - 1];
-        }
         if (!up(in.scalars, bs, 8)) return fail(MSM_ERR_HIP);
-        for (uint32_t m = 0; m < nm && !shared; m++) {
+        for (uint32_t m = 0; m < nreal && !shared; m++) {
           const size_t len = len_of(std::min(j * nm + m, count - 1));
           if (len < n) {
             hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
