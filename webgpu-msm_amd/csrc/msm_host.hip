@@ -1345,13 +1345,13 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
   const size_t G = std::min<size_t>(16, n / host_piece());
-  const size_t s = (n + G - 1) / G;  // (G - 1) s < n for G <= 16 <= sqrt(n): every slice is non-empty
+  const size_t s = (n + G - 1) / G;  // slices of s points; only the last is short (for n >= 2^18)
   std::vector<const uint32_t*> pp(G), ss(G);
   std::vector<size_t> lens(G);
   for (size_t g = 0; g < G; g++) {
     pp[g] = points_be + g * s * 32;
     ss[g] = scalars_be + g * s * 8;
-    lens[g] = std::min(s, n - g * s);
+    lens[g] = g * s < n ? std::min(s, n - g * s) : 0;  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
   }
   ManyInputs in;
   in.kind = ManyInputs::HOST;
