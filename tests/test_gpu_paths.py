@@ -209,6 +209,25 @@ def test_serial_flag_and_profile():
     assert 0 < prof["accumulate_sum"] / prof["profiled"] < 50.0
 
 
+def test_eight_msms_per_launch_small_sizes():
+    # up to 2^16 a count that fills eight-MSM launches runs eight per launch (padding MSMs of a
+    # short last launch otherwise); every result bit-exact
+    n = (1 << 16) - 3
+    d_pts = _dev(M.gen_points(n, k0=3, step=2))
+    scs = [M.gen_scalars(n, seed=1300 + j) for j in range(16)]
+    exps = [closed_form(3, 2, s) for s in scs]
+    M.set_profiling(2)
+    try:
+        out = M.compute_msm_many_device([d_pts] * 16, [_dev(s) for s in scs], n, flags=M.MSM_FLAG_SERIAL)
+        prof = M.last_profile()
+    finally:
+        M.set_profiling(False)
+    assert [as_xy(r) for r in out] == exps
+    assert prof["msms_per_launch"] == 8 and prof["profiled"] == 2
+    out = M.compute_msm_many([M.gen_points(n, k0=3, step=2)] * 13, scs[:13], n)  # 13 % 8 > 4: eight
+    assert [as_xy(r) for r in out] == exps[:13]
+
+
 def test_beyond_2_20_all_entries():
     # 2^21 + 17 points: one MSM per launch in the pipelined plan, L = 8 reduction for a lone MSM,
     # the host path as 16 slices plus a remainder; device, pipelined and host entries agree with

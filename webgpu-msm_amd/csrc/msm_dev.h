@@ -15,7 +15,7 @@ namespace msm {
 // A launch may carry a BATCH of nm independent MSMs of n points each (small MSMs fill the machine
 // together): MSM m owns windows [m Wm, (m+1) Wm) and point records [m n, (m+1) n); every kernel
 // after the recode sees W = nm Wm windows and does not care which MSM a window belongs to.
-constexpr uint32_t MSM_MAX_BATCH = 4;
+constexpr uint32_t MSM_MAX_BATCH = 8;
 struct BatchPtrs {  // per-MSM input buffers of a batch (kernel argument, by value)
   const uint32_t* p[MSM_MAX_BATCH];
 };
