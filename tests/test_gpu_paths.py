@@ -38,7 +38,7 @@ def test_host_entry_ragged_pieces():
 def test_host_entry_split_into_slices(n):
     # msm_compute from host arrays at n >= 2^18 runs G point-slices through the pipelined entry
     # (slice g+1 uploads while slice g computes) and joins the partials; n not a multiple of G
-    # leaves a remainder MSM of < G points
+    # leaves the last slice short, padded on the device (identity points, zero scalars)
     pts = M.gen_points(n, k0=3, step=5)
     sc = M.gen_scalars(n, seed=41 + n % 7)
     exp = closed_form(3, 5, sc)
@@ -49,14 +49,15 @@ def test_host_entry_split_into_slices(n):
 
 def test_host_split_projective_points():
     # the split host path with projective points (z != 1, normalised by k_prepare_points) in one
-    # launch's slices and in the remainder MSM; z = 0 in another launch is still rejected
+    # launch's slices and in the short, device-padded last slice; z = 0 in another launch is still
+    # rejected
     from oracle import oracle as O
 
-    n = (1 << 19) + 5  # four slices in two launches, and a one-point remainder
+    n = (1 << 19) + 5  # four slices in two launches, the last one short
     pts = M.gen_points(n, k0=9, step=7)
     sc = M.gen_scalars(n, seed=77)
     exp = closed_form(9, 7, sc)
-    # projective points in launch 0 (slices 0 and 1) and in the remainder
+    # projective points in launch 0 (slices 0 and 1) and at the end of the short last slice
     for i, z in ((3, 2), ((1 << 17) + 11, 12345678901), (n - 1, O.P - 2)):
         x, y, t = (O.be_words_to_int(pts[i, 8 * j: 8 * j + 8]) for j in range(3))
         for j, v in enumerate((x * z % O.P, y * z % O.P, t * z % O.P, z)):
@@ -230,7 +231,7 @@ def test_eight_msms_per_launch_small_sizes():
 
 def test_beyond_2_20_all_entries():
     # 2^21 + 17 points: one MSM per launch in the pipelined plan, L = 8 reduction for a lone MSM,
-    # the host path as 16 slices plus a remainder; device, pipelined and host entries agree with
+    # the host path as 16 slices, the last short and padded; device, pipelined and host entries agree with
     # the closed form
     n = (1 << 21) + 17
     pts = M.gen_points(n, k0=11, step=7)
