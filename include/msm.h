@@ -38,13 +38,39 @@ extern "C" {
 #define MSM_STREAM_NULL ((void*)1)
 
 /* msm_opts.flags */
-#define MSM_FLAG_SERIAL 1u /* pipelined entries: one launch in flight at a time (no overlap)     */
+#define MSM_FLAG_SERIAL 1u  /* pipelined entries: one launch in flight at a time (no overlap)     */
+#define MSM_FLAG_DEVICES 2u /* the device-list fields (devices, n_devices) are set: see below     */
 
+#define MSM_MAX_DEVICES 16
+
+/* Options.  The struct is versioned by its flags: the first four fields are the original
+ * (16-byte) layout, and a caller that never sets MSM_FLAG_DEVICES may pass that shorter struct --
+ * the library reads `devices` / `n_devices` only when the flag is set.
+ *
+ * Device list (MSM_FLAG_DEVICES; SURVEY.md §8b's "device mask, n_gpus"): the MSM runs on the
+ * `n_devices` listed gfx950 HIP ordinals (distinct, 1..MSM_MAX_DEVICES; `device` is ignored).  It
+ * generalises the reference's only sharding precedent, the CPU/GPU split inside one compute_msm
+ * call (submission.ts:116-154 + gpu_worker.ts:9-18, joined by point_add_affine lib.rs:240-253):
+ *   - msm_compute / msm_compute_partial: the point vector is cut into n_devices contiguous shards
+ *     (shard d = [n d / D, n (d+1) / D)), each device uploads and reduces its own shard on its own
+ *     host thread (its own PCIe link), and the shards' partials are joined with one EC add each;
+ *   - msm_compute_device / msm_compute_device_partial: the inputs live on one device (where the
+ *     pointers were allocated, which must be listed); the other listed devices copy their shard
+ *     from it over xGMI (peer copies) and reduce it, and the partials are joined the same way;
+ *   - msm_compute_many / msm_compute_shared (host batches): each device takes a contiguous block
+ *     of the `count` MSMs (no join: whole MSMs per device, the prover-batch replicas).
+ * The result is the same group element whatever the list (tests/test_gpu_multidev.py).  A
+ * repeated, negative or non-gfx950 ordinal, an empty list or more than MSM_MAX_DEVICES entries
+ * give MSM_ERR_INVALID_ARG; the list is checked before any work is enqueued. */
 typedef struct msm_opts {
   uint32_t window_bits; /* 0 = auto (msm_best_window); else 4..20. Replaces ?windowSize (submission.ts:29-33) */
   uint32_t run_length;  /* sorted-list entries per accumulation lane; 0 = auto                     */
   int32_t device;       /* HIP device ordinal (a gfx950 one), -1 = the calling thread's current device */
   uint32_t flags;       /* MSM_FLAG_* (0 = defaults)                                              */
+  /* --- read only when flags & MSM_FLAG_DEVICES --- */
+  const int32_t* devices; /* n_devices HIP ordinals                                                */
+  uint32_t n_devices;
+  uint32_t reserved; /* 0 */
 } msm_opts;
 
 /* Per-phase device times (ms) of the most recent MSM on the calling thread's device when
@@ -68,7 +94,11 @@ typedef struct msm_profile_t {
  * it probes the devices and fails with MSM_ERR_NO_DEVICE when no gfx950 is present. */
 int msm_init(void);
 void msm_shutdown(void);
+/* Number of gfx950 devices visible, and the HIP ordinal of the index-th of them (0-based; -1 when
+ * out of range).  On a node that mixes GPU types the gfx950 ordinals need not be contiguous, so
+ * callers mapping a rank or a list index to opts.device / opts.devices should go through it. */
 int msm_device_count(void);
+int msm_device_ordinal(int index);
 const char* msm_strerror(int code);
 
 /* getBestWindowSize (submission.ts:18-23), re-tuned for signed digits on MI355X. */

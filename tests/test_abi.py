@@ -51,7 +51,7 @@ def test_addon_exports():
         script = f"const a = require({addon!r}); console.log(Object.keys(a).sort().join(','))"
         keys = subprocess.run([node, "-e", script], capture_output=True, text=True, check=True).stdout.strip()
         assert keys.split(",") == sorted(["computeMsmU32", "computeMsmBigInt", "pointAddAffine", "split",
-                                          "bestWindowSize", "init", "deviceCount", "strerror"])
+                                          "bestWindowSize", "init", "deviceCount", "deviceOrdinals", "strerror"])
 
 
 def test_init_reports_device_state():
@@ -114,3 +114,49 @@ def test_generators_match_oracle():
     assert np.array_equal(M.gen_points(300, k0=5, step=9), O.gen_points(300, k0=5, step=9))
     assert np.array_equal(M.gen_points(5000), O.gen_points(5000))
     assert np.array_equal(M.gen_scalars(777, seed=3), O.xorshift_scalars_np(777, seed=3))
+
+
+def test_opts_struct_layout_matches_header():
+    """msm_opts: the original 16-byte layout, then the device list (include/msm.h)."""
+    src = open(HEADER).read()
+    body = src[src.index("typedef struct msm_opts {"):src.index("} msm_opts;")]
+    fields = re.findall(r"^\s*(?:const\s+)?([a-z0-9_]+\*?)\s*(\*?)([a-z_]+);", body, flags=re.M)
+    assert [f[2] for f in fields] == [n for n, _ in M.MsmOpts._fields_]
+    assert ctypes.sizeof(M.MsmOpts) == 32
+    assert M.MsmOpts.devices.offset == 16 and M.MsmOpts.n_devices.offset == 24
+    flags = dict(re.findall(r"#define (MSM_FLAG_[A-Z]+) (\d+)u", src))
+    assert int(flags["MSM_FLAG_SERIAL"]) == M.MSM_FLAG_SERIAL and int(flags["MSM_FLAG_DEVICES"]) == M.MSM_FLAG_DEVICES
+    assert int(re.search(r"#define MSM_MAX_DEVICES (\d+)", src).group(1)) == M.MSM_MAX_DEVICES
+
+
+@pytest.mark.parametrize("devices", [[], [0, 0], [-1], [1, 2, 1], list(range(17))])
+def test_bad_device_lists_rejected_before_any_device_work(devices):
+    """Shape errors in a device list are MSM_ERR_INVALID_ARG whether or not a GPU is present."""
+    pts, sc = O.gen_points(4), O.ints_to_be_words([1, 2, 3, 4])
+    for call in (lambda: M.compute_msm_wire(pts, sc, devices=devices),
+                 lambda: M.compute_msm_partial(pts, sc, devices=devices),
+                 lambda: M.compute_msm_many([pts], [sc], 4, devices=devices),
+                 lambda: M.compute_msm_shared(pts, [sc], 4, devices=devices)):
+        with pytest.raises(M.MsmError) as e:
+            call()
+        assert e.value.code == -1
+
+
+def test_null_device_list_rejected():
+    L = M.load()
+    o = M.MsmOpts(0, 0, -1, M.MSM_FLAG_DEVICES)
+    o.n_devices = 2  # devices left NULL
+    out = (ctypes.c_uint32 * 16)()
+    pts, sc = O.gen_points(2), O.ints_to_be_words([1, 2])
+    assert L.msm_compute(pts.ctypes.data, sc.ctypes.data, 2, ctypes.byref(o), out) == -1
+
+
+def test_device_ordinals_consistent():
+    L = M.load()
+    n = L.msm_device_count()
+    assert M.device_ordinals() == [L.msm_device_ordinal(i) for i in range(n)]
+    assert L.msm_device_ordinal(-1) == -1 and L.msm_device_ordinal(n) == -1
+    if n == 0:  # no GPU here: a well-formed list fails loudly with MSM_ERR_NO_DEVICE
+        with pytest.raises(M.MsmError) as e:
+            M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]), devices=[0])
+        assert e.value.code == -6

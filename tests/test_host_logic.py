@@ -1,4 +1,5 @@
 """Host-side marshalling and the TypeScript/JS surface (node), CPU only."""
+import ctypes
 import json
 import os
 import shutil
@@ -146,3 +147,40 @@ def test_red1_lane_map_is_a_bijection_live_first():
                         assert live, (c, nm, L, w, ch)
                 assert len(seen) == Wm * nm * nchunks
                 assert _red1_lane(Wm, nm, nhi, B, L, nchunks, Wm * nm * nchunks) is None
+
+
+def _shard(n, i, D):
+    L = M.load()
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    assert L.msm_test_shard_range(n, i, D, ctypes.byref(lo), ctypes.byref(hi)) == 0
+    return lo.value, hi.value
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 1 << 20, (1 << 20) + 5])
+def test_device_shards_partition_the_points(n):
+    """The device-list split (msm_opts MSM_FLAG_DEVICES) is contiguous, covers [0, n), sizes
+    differ by at most one, and agrees with the torch.distributed split (msm_amd.dist)."""
+    from msm_amd.dist import shard_range
+    for D in range(1, M.MSM_MAX_DEVICES + 1):
+        spans = [_shard(n, i, D) for i in range(D)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(D - 1))
+        sizes = [hi - lo for lo, hi in spans]
+        assert max(sizes) - min(sizes) <= 1
+        assert spans == [shard_range(n, i, D) for i in range(D)]
+
+
+def test_device_shard_join_equals_whole_msm():
+    """Shard partials (closed form per shard) joined by libmsm's host EC adds = the whole MSM."""
+    from _closed_form import closed_form
+    n = 1001
+    sc = O.xorshift_scalars_np(n, seed=77)
+    whole = closed_form(3, 5, sc)
+    for D in (1, 2, 3, 8, 16):
+        parts = np.zeros((D, 32), np.uint32)
+        for i in range(D):
+            lo, hi = _shard(n, i, D)
+            x, y = closed_form(3 + 5 * lo, 5, sc[lo:hi]) if hi > lo else O.IDENTITY
+            for j, v in enumerate((x, y, x * y % O.P, 1)):
+                parts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
+        assert M.combine_partials(parts) == whole

@@ -42,26 +42,64 @@ def value_of(limbs):
     return sum(x << (LB * i) for i, x in enumerate(limbs))
 
 
-def fe_mul(a: B, b: B) -> B:
-    assert a.v * b.v < P * R, "lazy Montgomery output would exceed 2p"
+WIDE_ALL, WIDE_GH, WIDE_EH = 0xFF, 0xE7, 0xBF  # fp29.cuh: steps with a 32-bit reduction digit
+
+
+def seed(wide: int, k: int) -> int:
+    """fp29.cuh fe_mul_seed: register offset of column k (2^32 - 1 on the reduction columns, -7
+    after a narrow step)."""
+    return ((1 << 32) - 1 if k <= NL - 1 else 0) - (7 if k >= 1 and not (wide >> (k - 1)) & 1 else 0)
+
+
+def digit_max(wide: int, i: int) -> int:
+    return (1 << 32) - 1 if i < NL - 1 and (wide >> i) & 1 else (1 << LB) - 1
+
+
+def fe_mul(a: B, b: B, wide: int = WIDE_ALL) -> B:
+    # the digits add sum_i m_i 2^(29 i) p to the product before the division by R
+    extra = sum(digit_max(wide, i) << (LB * i) for i in range(NL)) * P
+    assert a.v * b.v + extra < 2 * P * R, "lazy Montgomery output would exceed 2p"
     cols = [0] * (2 * NL)
     for i in range(NL):
         for j in range(NL):
             cols[i + j] += a.l[i] * b.l[j]
-    cols[NL] += 1  # the one seeded product (the last reduction step's carry +1)
     carry = 0
     for k in range(2 * NL):
-        red = 0
-        for i in range(NL):  # reduction digits m_i <= 2^29 times P29[k - i], k - i in 1..8
-            j = k - i
-            if 1 <= j < NL and i < NL:
-                red += (1 << LB) * P29[j]
-        # columns 1..8 hold their value minus the (un-added) +1 of the incoming carry, which is
-        # <= the true column, so bounding the true column (carry + 1) bounds the register too
+        red = sum(digit_max(wide, i) * P29[k - i] for i in range(NL) if 1 <= k - i < NL)
+        # the register: true column (products + reduction terms + incoming carry) + its seed
         col = cols[k] + red + carry
-        assert col < 1 << 64, f"column {k} may reach {col / 2**64:.3f} * 2^64"
-        carry = (col >> LB) + 1
+        assert col + max(0, seed(wide, k)) < 1 << 64, f"column {k} may reach {col / 2**64:.3f} * 2^64"
+        # carry out: (column + digit) / 2^29 on the reduction columns, column >> 29 above
+        carry = (col + digit_max(wide, k)) >> LB if k < NL else col >> LB
     return N_MUL
+
+
+def fe_mul_exact(a, b, wide: int = WIDE_ALL):
+    """Bit-exact model of fp29.cuh fe_mul_w<wide> on limb lists (64-bit register wrap checked):
+    returns the 9 output limbs."""
+    M64 = (1 << 64) - 1
+    c = [0] * (2 * NL)
+    for k in range(NL + 1):
+        c[k] = seed(wide, k) & M64
+    for i in range(NL):
+        for j in range(NL):
+            c[i + j] = (c[i + j] + a[i] * b[j]) & M64
+    for i in range(NL):
+        lo = c[i] & 0xFFFFFFFF
+        if i < NL - 1 and (wide >> i) & 1:
+            m = ~lo & 0xFFFFFFFF
+            c[i + 1] = (c[i + 1] + 8 * (c[i] >> 32)) & M64
+        else:
+            m = ~lo & MASK
+            c[i + 1] = (c[i + 1] + (c[i] >> LB)) & M64
+        for j in range(1, NL):
+            c[i + j] = (c[i + j] + m * P29[j]) & M64
+    r = [0] * NL
+    for k in range(NL, 2 * NL - 1):
+        c[k + 1] = (c[k + 1] + (c[k] >> LB)) & M64
+        r[k - NL] = c[k] & MASK
+    r[NL - 1] = c[2 * NL - 1] & 0xFFFFFFFF
+    return r
 
 
 K2D_INT, MU2D = 6042, (1 << 284) // P
@@ -146,12 +184,12 @@ def test_madd_bounds():
         G = fe_add(D, C)
         H = fe_add(Bv, A)
         fe_mul(E, F)
-        fe_mul(G, H)
-        fe_mul(E, H)
+        fe_mul(G, H, WIDE_GH)
+        fe_mul(E, H, WIDE_EH)
         fe_mul(F, G)
 
 
-def test_padd_bounds():
+def padd_operands():
     p = q = PT
     A = fe_mul(fe_sub_u(p["Y"], p["X"]), fe_sub(q["Y"], q["X"]))
     Bv = fe_mul(fe_add(p["Y"], p["X"]), fe_add(q["Y"], q["X"]))
@@ -162,9 +200,14 @@ def test_padd_bounds():
     F = fe_sub(D, C)
     G = fe_add(D, C)
     H = fe_add(Bv, A)
+    return E, F, G, H
+
+
+def test_padd_bounds():
+    E, F, G, H = padd_operands()
     fe_mul(E, F)
-    fe_mul(G, H)
-    fe_mul(E, H)
+    fe_mul(G, H, WIDE_GH)
+    fe_mul(E, H, WIDE_EH)
     fe_mul(F, G)
 
 
@@ -188,8 +231,54 @@ def test_mul_2d_exact_and_bounded():
 
 def test_quad_add_bounds():
     # pt_add_quad: round 1 A | B | T1T2 | Z1Z2 on the four lanes, C = fe_mul_2d(T1T2) on lane 2,
-    # then EF | GH | EH | FG -- the same operands as pt_add
-    test_padd_bounds()
+    # then EF | GH | EH | FG -- the same operands as pt_add, through one multiply whose wide steps
+    # suit all four (WIDE_GH & WIDE_EH)
+    E, F, G, H = padd_operands()
+    for a, b in ((E, F), (G, H), (E, H), (F, G)):
+        fe_mul(a, b, WIDE_GH & WIDE_EH)
+
+
+def test_wide_masks_are_maximal():
+    """The masks in fp29.cuh are the widest the column budget allows for their operand forms."""
+    N = N_MUL
+    G, H, E = fe_add(fe_add(N, N), N), fe_add(N, N), fe_sub_u(N, N)
+    for (a, b), mask in (((G, H), WIDE_GH), ((E, H), WIDE_EH)):
+        fe_mul(a, b, mask)
+        for extra in range(8):
+            if not (mask >> extra) & 1:
+                try:
+                    fe_mul(a, b, mask | 1 << extra)
+                except AssertionError:
+                    continue
+                raise AssertionError(f"mask {mask:#x} could also widen step {extra}")
+
+
+def test_fe_mul_exact_model():
+    """Bit-exact model of fe_mul_w: a b R^-1 mod p, normalised limbs, value < 2p -- random
+    operands and operands at the limb maxima of each call site's forms."""
+    import random
+    rnd = random.Random(5)
+    Rinv = pow(R, -1, P)
+
+    def limbs_of(v):
+        return [(v >> (LB * i)) & MASK for i in range(NL - 1)] + [v >> (LB * (NL - 1))]
+
+    cases = []
+    for _ in range(3000):
+        cases.append((limbs_of(rnd.randrange(2 * P)), limbs_of(rnd.randrange(2 * P)), rnd.choice(
+            (WIDE_ALL, WIDE_GH, WIDE_EH, WIDE_GH & WIDE_EH, 0))))
+    # unnormalised operands at their forms' maxima (value = sum of limbs 2^(29 i), kept < 2^257)
+    top = (1 << 257) >> (LB * (NL - 1))
+    s_max = [(1 << 30) - 1] * (NL - 1) + [top // 2]
+    g_max = [3 * (1 << 29) // 2] * (NL - 1) + [top // 4]
+    u_max = [x + k - 1 for x, k in zip([0] * NL, K8P29)]
+    for a, b, w in ((g_max, s_max, WIDE_GH), (u_max, s_max, WIDE_EH), (s_max, s_max, WIDE_ALL)):
+        cases.append((a, b, w))
+    for a, b, w in cases:
+        r = fe_mul_exact(a, b, w)
+        v = value_of(r)
+        assert v % P == value_of(a) * value_of(b) * Rinv % P
+        assert v < 2 * P and all(x <= MASK for x in r[:NL - 1])
 
 
 def test_pdbl_bounds():
@@ -227,7 +316,9 @@ _CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REVIEWED = {
     ("fp29.cuh", "mad64"): "b50540a0d8a64ede",
     ("fp29.cuh", "seeded"): "d5de263bcd90d0e8",
-    ("fp29.cuh", "fe_mul"): "e89342f9ea9e59ca",
+    ("fp29.cuh", "fe_mul"): "cb1d67f3d0051cb5",
+    ("fp29.cuh", "fe_mul_w"): "9fc551211780fac2",
+    ("fp29.cuh", "fe_mul_seed"): "d98e5e7e34126a6e",
     ("fp29.cuh", "fe_norm"): "37b756e7bd4474d2",
     ("fp29.cuh", "fe_add"): "d14b6a137a6ff34d",
     ("fp29.cuh", "fe_add_n"): "bdf7dd24032e38f7",
@@ -238,11 +329,11 @@ REVIEWED = {
     ("fp29.cuh", "fe_mul_2d"): "b9f5c6afdcbc7ff4",
     ("fp29.cuh", "P29"): "b4babf5a3c9d7331",
     ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
-    ("ec.cuh", "pt_madd"): "bca5cd1691b5dc73",
-    ("ec.cuh", "pt_add"): "8b71b3f9aba1c9c2",
+    ("ec.cuh", "pt_madd"): "105059873268fc45",
+    ("ec.cuh", "pt_add"): "c6352f37d81bec89",
     ("ec.cuh", "pt_dbl"): "784353f9934ef437",
     ("ec.cuh", "pre_neg_if"): "a318c90204dc7c80",
-    ("ec.cuh", "pt_add_quad"): "2c7df2e0c3aa2b85",
+    ("ec.cuh", "pt_add_quad"): "875eba21c1f11e82",
 }
 
 
@@ -268,3 +359,9 @@ def test_mirrored_sources_unchanged():
     changed = {f"{f}:{n}": _body_digest(f, n) for (f, n), d in REVIEWED.items() if _body_digest(f, n) != d}
     assert not changed, ("device code mirrored by this proof changed -- re-check the formulas above, then update "
                          f"REVIEWED with: {changed}")
+
+
+def test_wide_mask_constants_match_header():
+    src = open(os.path.join(_CSRC, "fp29.cuh")).read()
+    got = {k: int(v, 16) for k, v in re.findall(r"constexpr uint32_t (WIDE_[A-Z]+) = (0x[0-9A-Fa-f]+)u;", src)}
+    assert got == {"WIDE_ALL": WIDE_ALL, "WIDE_GH": WIDE_GH, "WIDE_EH": WIDE_EH}

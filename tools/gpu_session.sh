@@ -1,0 +1,87 @@
+#!/bin/bash
+# One parametrised GPU session (replaces the round-2 one-off session scripts).  Run on the GPU box:
+#
+#   bash tools/gpu_session.sh <tag> <step> [<step> ...]
+#
+# Every step runs under its own time limit; its output goes to gpurun_out/<tag>_<step>.txt (or a
+# directory of that name for profiles), and the session stops at the first step that crashes,
+# times out or fails (no GPU step after a fault).  Steps:
+#   tests        the -m gpu parity suites (libmsm.so)
+#   tests_alt    the same with eager launches, then with one slot and one MSM per launch
+#   bench        python bench.py (the driver's command)
+#   bench50      50 timed steps, no extras
+#   sizes        pipelined ms per MSM at 2^16..2^19 (20 and 50 steps)
+#   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
+#   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
+#   multidev     bench.py --multi-device: msm_compute over every visible device in one process
+#   kstats       rocprofv3 --kernel-trace --stats of the default bench command
+#   kstats1      the same on one stream (MSM_SLOTS=1), two-MSM 2^20 launches only
+#   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
+#   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
+#                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
+#   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
+set -u
+[ $# -ge 2 ] || { sed -n 2,24p "$0"; exit 2; }
+TAG=$1; shift
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+LIBDIR=$PWD/webgpu-msm_amd/msm_amd/_lib
+BENCH_Q=(--no-cpu-baseline)
+
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  local out=gpurun_out/${TAG}_$name.txt
+  echo "== $name: $*" >&2
+  timeout -k 10 "$to" "$@" > "$out" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(grep -ao '"value": [0-9.]*\|[0-9]* passed[^=]*\|[0-9]* failed' "$out" | head -2 | tr '\n' ' ')" >&2
+  if [ $rc -ne 0 ]; then
+    tail -n 20 "$out" >&2
+    echo "ABORT after $name (rc=$rc)" >&2
+    exit $rc
+  fi
+}
+
+pytest_gpu() { python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread "$@"; }
+
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 pytest_gpu ;;
+    tests_alt)
+      MSM_NO_GRAPH=1 run tests_eager 900 pytest_gpu -k "not random_sweep"
+      MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 pytest_gpu -k "not random_sweep" ;;
+    bench) run bench 300 python bench.py ;;
+    bench50) run bench50 300 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" ;;
+    sizes)
+      for lg in 16 17 18 19; do
+        run size$lg 120 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
+        run size${lg}_k20 120 python bench.py --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
+      done ;;
+    batch64) run batch64 300 python bench.py --batch 64 --n 262144 ;;
+    gloo8)
+      MSM_DIST_BACKEND=gloo OMP_NUM_THREADS=2 run gloo8 400 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 2 \
+        --no-extras "${BENCH_Q[@]}" ;;
+    multidev) run multidev 300 python bench.py --multi-device --no-extras "${BENCH_Q[@]}" ;;
+    kstats)
+      run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
+        -- python3 bench.py ;;
+    kstats1)
+      MSM_SLOTS=1 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
+        -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 20 --warmup 4 --serial-min-s 0 ;;
+    pmc) run pmc 900 bash tools/profile_pmc.sh "$TAG" ;;
+    ab:*)
+      IFS=: read -r _ libs rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-3}"); do
+        for lib in ${libs//,/ }; do
+          MSM_AMD_LIB=$LIBDIR/$lib run "ab_${lib%.so}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+        done
+      done ;;
+    ubench)
+      run ubench_fmul 120 tools/ubench/fmul_bench
+      run ubench_isa 120 tools/ubench/isa_rates ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+echo "== session $TAG done" >&2

@@ -1,11 +1,14 @@
 """Static instruction mix of k_accumulate's hot loop (the one-entry mixed-add block) and the VALU
 issue cycles it demands per wave-iteration on gfx950.
 
-    python tools/isa_mix.py [--out profiles/r2_isa_mix.json]
+    python tools/isa_mix.py --asm <device .s> --lib <libmsm.so> --out <libmsm.isa.json>   (make)
+    python tools/isa_mix.py --out <json>          (compiles its own copy with --save-temps)
 
-Compiles libmsm's device code with --save-temps into a scratch directory, takes the basic block
-of k_accumulate holding the most 64-bit multiply-adds (one pt_madd per wave-iteration), and prices it
-two ways:
+The Makefile builds libmsm.so with -save-temps and runs this on the device assembly of that same
+compile, recording the shipped library's sha256: the assembly is what the code object inside
+that .so was assembled from, so bench.py's ISA floor belongs to the library it loads (it checks
+the hash and reports no floor on a mismatch).  The basic block of k_accumulate holding the most
+64-bit multiply-adds (one pt_madd per wave-iteration) is priced two ways:
   * cycles_per_iteration: the nominal gfx950 model (a SIMD-32 issues a 32-bit VALU wave64
     instruction in 2 cycles, a 64-bit one -- v_mad_u64_u32, 64-bit shifts/adds/moves -- in 4);
   * ns_per_iteration_chip: every instruction at the chip-wide issue rate MEASURED for it (or its
@@ -94,12 +97,18 @@ def base(op):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_isa_mix.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "webgpu-msm_amd", "msm_amd", "_lib", "libmsm.isa.json"))
     ap.add_argument("--func", default="k_accumulate")
     ap.add_argument("--rates", default=os.path.join(ROOT, "profiles", "r2_isa_rates.json"))
+    ap.add_argument("--asm", help="device assembly of the library build (-save-temps); default: compile a copy")
+    ap.add_argument("--lib", help="the library that assembly was linked into (its sha256 is recorded)")
     args = ap.parse_args()
-    with tempfile.TemporaryDirectory() as tmp:
-        blocks, loops = blocks_of(asm_text(tmp), args.func)
+    if args.asm:
+        with open(args.asm) as f:
+            blocks, loops = blocks_of(f.read(), args.func)
+    else:
+        with tempfile.TemporaryDirectory() as tmp:
+            blocks, loops = blocks_of(asm_text(tmp), args.func)
     # the loop block with the most multiplies: one entry's pt_madd per wave-iteration
     name, ins = max(((k, v) for k, v in blocks.items() if k in loops),
                     key=lambda kv: sum(1 for o in kv[1] if o in MADS))
@@ -114,6 +123,11 @@ def main():
            "cycle_model": "gfx950 SIMD-32: 2 cycles per 32-bit VALU wave64 instruction, 4 per 64-bit one "
                           "(v_mad_u64_u32, 64-bit shifts/adds/moves); profiles/r2_isa_rates.json",
            "mix": dict(cnt.most_common())}
+    if args.lib:
+        import hashlib
+        with open(args.lib, "rb") as f:
+            res["lib_sha256"] = hashlib.sha256(f.read()).hexdigest()
+        res["lib"] = os.path.basename(args.lib)
     if os.path.exists(args.rates):
         ns, unpriced = price_measured(cnt, args.rates)
         res["ns_per_iteration_chip"] = ns

@@ -12,9 +12,11 @@
 // Laziness: R = 2^261 >> p, so the Montgomery product of any a, b < 2^257 (~16p) is < 2p and
 // needs no final subtraction.  Additions are limb-wise with no carry; subtractions add a
 // redundant multiple of p whose limbs dominate any normalised limb, then renormalise.
-// Limb-size rule for fe_mul(a, b): maxlimb(a) * maxlimb(b) <= 2^60 (then each 64-bit column
-// sum <= 9*2^60 + 9*2^58 + 2^35 < 2^64).  "N" = normalised (limbs < 2^29), "S" = sum of two N
-// (limbs < 2^30).  N*N, N*S, S*S are all legal.  Values entering fe_mul stay < 2^257.
+// Limb forms: "N" = normalised (limbs < 2^29), "S" = sum of two N (limbs < 2^30), "U" = an
+// unnormalised difference (limbs < 1.48 * 2^30).  Each 64-bit column holds up to 9 limb products
+// plus the reduction products (fe_mul_w: up to 2^32 * p_j), so which operand forms may meet is
+// decided per call site by tests/test_limb_bounds.py (every column < 2^64, worst case over the
+// per-limb maxima).  Values entering fe_mul stay < 2^257.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -83,32 +85,72 @@ __device__ __forceinline__ fe fe_zero() {
 __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 
 // Montgomery product a*b*2^-261 mod p (result normalised, value < 2p when a,b < 2^257).
-// Reduction digits, with p = 1 (mod 2^29) (so m * p_0 = m):
-//  * step 0: m_0 = 2^29 - (c_0 mod 2^29) in [1, 2^29]; it zeroes column 0 and carries exactly
-//    (c_0 >> 29) + 1.
-//  * steps 1..8 see their column "biased": the +1 of the previous carry is not added, so the
-//    register holds s_i = column_i - 1 (>= 0: every carry is >= 1).  Then m_i = ~s_i mod 2^29
-//    = 2^29 - 1 - (s_i mod 2^29) (one v_bfi_b32) again zeroes the column, whose carry is
-//    (s_i >> 29) + 1, and the +1 is again left as the next column's bias.
-//  * the last step's +1 lands in column 9 (the result's limb 0): one seeded product.
-// m_i <= 2^29 as before, so column bounds are unchanged (tests/test_limb_bounds.py).
-__device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
+//
+// Reduction digits (p = 1 mod 2^29, so m * p_0 = m).  Every reduction column k = 0..8 is seeded
+// with 2^32 - 1, so its register holds s_k = c_k + 2^32 - 1 (c_k = the true column, >= 0).  Step
+// k is one of two kinds (bit k of WIDE):
+//  * wide (k <= 7): a full 32-bit digit m_k = ~lo(s_k) (one v_not).  Then c_k + m_k = 2^32 hi(s_k)
+//    exactly, i.e. the column is zero to 32 bits and its carry into column k+1 (units of 2^29) is
+//    8 hi(s_k): ONE v_mad_u64_u32 (hi, 8, s_{k+1}) -- no 64-bit shift and add.
+//  * narrow: m_k = ~lo(s_k) mod 2^29 = 2^29 - 1 - ((c_k - 1) mod 2^29) zeroes the column to 29
+//    bits; its carry is (s_k >> 29) - 7, added as s_k >> 29 (64-bit shift + add) with the -7
+//    pre-seeded into column k+1.  The last step (k = 8) is always narrow: the digits' share of
+//    the result is sum_k m_k 2^(29k) p / 2^261, so a 32-bit m_8 would add up to 8p, while 32-bit
+//    digits below it add at most 2^-26 p -- the result stays < 2p.
+// A 32-bit digit makes its reduction products 8x larger, so the columns near the middle only fit
+// 64 bits for the narrower operand forms: WIDE_ALL for N/S/U x N operands (and S x S), fewer
+// wide steps for the two products of pt_madd / pt_add with an S operand against a 1.5-form or
+// U one (tests/test_limb_bounds.py proves every call site's columns < 2^64).
+#ifndef MSM_NARROW_DIGITS  // A/B builds only: -DMSM_NARROW_DIGITS gives every step a 29-bit digit
+constexpr uint32_t WIDE_ALL = 0xFFu;  // steps 0..7 wide
+constexpr uint32_t WIDE_GH = 0xE7u;   // steps 0, 1, 2, 5, 6, 7: G (< 1.5 * 2^30 limbs) x H (S)
+constexpr uint32_t WIDE_EH = 0xBFu;   // steps 0..5, 7:          E (U) x H (S)
+#else
+constexpr uint32_t WIDE_ALL = 0u, WIDE_GH = 0u, WIDE_EH = 0u;
+#endif
+
+__host__ __device__ constexpr uint64_t fe_mul_seed(uint32_t wide, int k) {
+  // column k's register offset: 2^32 - 1 for the reduction columns, minus 7 after a narrow step
+  return (k <= NL - 1 ? 0xFFFFFFFFull : 0ull) - ((k >= 1 && !((wide >> (k - 1)) & 1u)) ? 7ull : 0ull);
+}
+
+// An opaque 32-bit value held in an SGPR: the multiplier of the wide steps' carry product, so
+// LLVM keeps 8 hi(s) + s' one v_mad_u64_u32 instead of rewriting it as shifts and masks.
+__device__ __forceinline__ uint32_t opaque_s(uint32_t v) {
+  asm("" : "+s"(v));
+  return v;
+}
+
+template <uint32_t WIDE>
+__device__ __forceinline__ fe fe_mul_w(const fe& a, const fe& b) {
   uint64_t c[2 * NL];
+  const uint32_t eight = opaque_s(8u);
+  // Each column is one chain of multiply-adds starting from its seed.  Every link is pinned
+  // (seeded): LLVM's reassociation would otherwise sum the products first and add the seed (or
+  // the carry) with a separate 64-bit add.
 #pragma unroll
-  for (int k = 0; k < 2 * NL; k++) c[k] = 0;
-  c[NL] = seeded(mad64(a.v[1], b.v[NL - 1], 1));
+  for (int k = 0; k < NL; k++) c[k] = seeded(mad64(a.v[0], b.v[k], fe_mul_seed(WIDE, k)));
+  c[NL] = seeded(mad64(a.v[1], b.v[NL - 1], fe_mul_seed(WIDE, NL)));
 #pragma unroll
-  for (int i = 0; i < NL; i++)
+  for (int k = NL + 1; k < 2 * NL; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 1; i < NL; i++)
 #pragma unroll
     for (int j = 0; j < NL; j++) {
-      if (i == 1 && j == NL - 1) continue;  // issued above as the seeded product
-      c[i + j] = mad64(a.v[i], b.v[j], c[i + j]);
+      if (i == 1 && j == NL - 1) continue;  // issued above as a seeded product
+      c[i + j] = i + j > NL ? mad64(a.v[i], b.v[j], c[i + j]) : seeded(mad64(a.v[i], b.v[j], c[i + j]));
     }
 #pragma unroll
   for (int i = 0; i < NL; i++) {
     const uint32_t lo = (uint32_t)c[i];
-    const uint32_t m = i == 0 ? (1u << LBITS) - (lo & LMASK) : (~lo & LMASK);
-    c[i + 1] += c[i] >> LBITS;
+    uint32_t m;
+    if (i < NL - 1 && ((WIDE >> i) & 1u)) {
+      m = ~lo;
+      c[i + 1] = seeded(mad64((uint32_t)(c[i] >> 32), eight, c[i + 1]));
+    } else {
+      m = ~lo & LMASK;
+      c[i + 1] += c[i] >> LBITS;
+    }
 #pragma unroll
     for (int j = 1; j < NL; j++) c[i + j] = mad64(m, P29[j], c[i + j]);
   }
@@ -121,6 +163,9 @@ __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   r.v[NL - 1] = (uint32_t)c[2 * NL - 1];
   return r;
 }
+
+// Every operand pair but the S x (1.5 | U) products named above: all eight low digits wide.
+__device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) { return fe_mul_w<WIDE_ALL>(a, b); }
 
 __device__ __forceinline__ fe fe_sqr(const fe& a) { return fe_mul(a, a); }
 

@@ -225,7 +225,7 @@ std::mutex g_mu;
 std::vector<DevCtx*> g_ctx;   // indexed by HIP ordinal
 std::vector<int> g_gfx950;    // HIP ordinals of the gfx950 devices
 int g_nhip = -1;              // HIP devices visible (any architecture)
-int g_profiling = 0;
+std::atomic<int> g_profiling{0};  // read by calls on other devices' threads
 
 int probe_devices() {
   if (g_nhip >= 0) return (int)g_gfx950.size();
@@ -1071,11 +1071,18 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   sl.pl = pl;
   uint32_t* pts = w.pts.as<uint32_t>();
   const BatchPtrs bp = splat(w.wire_pts.as<uint32_t>()), bs = splat(w.wire_sc.as<uint32_t>());
-  if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK) return rc;
-  if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return rc;
+  // once an upload is queued, an error return first waits for it: the copies read the caller's
+  // arrays, which msm.h promises are not read after the call returns
+  auto fail = [&](int code) {
+    hipStreamSynchronize(c->copy_stream);
+    hipStreamSynchronize(sl.stream);
+    return code;
+  };
+  if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK) return fail(rc);
+  if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
   if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
-    return rc;
-  if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return rc;
+    return fail(rc);
+  if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return fail(rc);
   return finish_msm(c, si, result);
 }
 
@@ -1157,7 +1164,9 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   const bool host = in.kind == ManyInputs::HOST;
   for (size_t b = 0; b < count; b++)
     if ((!shared && !in.points[b]) || !in.scalars[b]) return MSM_ERR_INVALID_ARG;
-  const uint32_t nm = in.batch ? (uint32_t)std::min<size_t>(in.batch, count) : pipeline_batch(n, count);
+  // the batch's BatchPtrs hold MSM_MAX_BATCH entries: never more MSMs per launch than that
+  const uint32_t nm = (uint32_t)std::min<size_t>(
+      in.batch ? std::min<size_t>(in.batch, count) : pipeline_batch(n, count), MSM_MAX_BATCH);
   const size_t nbatch = (count + nm - 1) / nm;
   Plan pl;
   int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm, shared);
@@ -1321,7 +1330,7 @@ int on_device(const msm_opts* opts, F&& fn) {
   if (rc != MSM_OK) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  c->profiling = g_profiling;
+  c->profiling = g_profiling.load();
   begin_call(c);
   rc = fn(c);
   end_call(c);
@@ -1333,9 +1342,9 @@ size_t host_piece() {
   static const size_t v = getenv("MSM_HOST_PIECE_LOG") ? (size_t)1 << atoi(getenv("MSM_HOST_PIECE_LOG")) : (size_t)1 << 17;
   return v;
 }
-uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices (profiles/r2kl_*)
-  static const uint32_t v = getenv("MSM_HOST_NM") ? (uint32_t)atoi(getenv("MSM_HOST_NM")) : 2u;
-  return v;
+uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
+  static const int env = getenv("MSM_HOST_NM") ? atoi(getenv("MSM_HOST_NM")) : 2;
+  return (uint32_t)std::min(std::max(env, 1), (int)MSM_MAX_BATCH);
 }
 
 // One large MSM of host-resident inputs as G point-slices (G <= 16, slices of >= 2^17 points):
@@ -1398,6 +1407,182 @@ int many_entry(const ManyInputs& in, size_t n, size_t count, const msm_opts* opt
   });
 }
 
+// ---- several devices in one call (msm_opts.flags & MSM_FLAG_DEVICES, include/msm.h) ----------
+// The reference's one sharding precedent is inside compute_msm: the point vector split between
+// the CPU and the GPU worker (submission.ts:116-154, gpu_worker.ts:9-18) and the two partials
+// joined with point_add_affine (lib.rs:240-253).  Here the split is over gfx950 devices, one
+// host thread each, and the join is projective (one EC add per shard, one inversion at the end).
+
+bool devices_listed(const msm_opts* o) { return o && (o->flags & MSM_FLAG_DEVICES); }
+
+// The listed ordinals, checked for shape (non-null, 1..MSM_MAX_DEVICES entries, non-negative,
+// distinct) before any device is touched, then for being gfx950 devices.
+int device_list(const msm_opts* o, std::vector<int>* devs) {
+  devs->clear();
+  if (!o->devices || o->n_devices == 0 || o->n_devices > MSM_MAX_DEVICES) return MSM_ERR_INVALID_ARG;
+  for (uint32_t i = 0; i < o->n_devices; i++) {
+    const int d = o->devices[i];
+    if (d < 0 || std::find(devs->begin(), devs->end(), d) != devs->end()) return MSM_ERR_INVALID_ARG;
+    devs->push_back(d);
+  }
+  for (int d : *devs) {
+    DevCtx* c;
+    if (int rc = get_ctx(d, &c)) return rc;
+  }
+  return MSM_OK;
+}
+
+// One listed device's single-device options.
+msm_opts opts_on(const msm_opts* o, int device) {
+  msm_opts r{};
+  r.window_bits = o->window_bits;
+  r.run_length = o->run_length;
+  r.flags = o->flags & ~MSM_FLAG_DEVICES;
+  r.device = device;
+  return r;
+}
+
+// Contiguous shard i of D over n items: [n i / D, n (i+1) / D) (sizes differ by at most one).
+void shard_range(size_t n, size_t i, size_t D, size_t* lo, size_t* hi) {
+  *lo = n * i / D;
+  *hi = n * (i + 1) / D;
+}
+
+// fn(i) for every listed device, device i on its own host thread (device 0 on the caller's); the
+// first error in list order is returned once all have finished.
+template <typename F>
+int for_each_device(size_t D, F&& fn) {
+  std::vector<int> rc(D, MSM_OK);
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < D; i++) th.emplace_back([&, i] { rc[i] = fn(i); });
+  rc[0] = fn(0);
+  for (std::thread& t : th) t.join();
+  for (int r : rc)
+    if (r != MSM_OK) return r;
+  return MSM_OK;
+}
+
+Pt join_partials(const std::vector<Pt>& part) {
+  Pt acc = part[0];
+  for (size_t i = 1; i < part.size(); i++) acc = pt_add(acc, part[i]);
+  return acc;
+}
+
+// msm_compute / msm_compute_partial: each listed device uploads and reduces its own shard.
+// (`devs` may repeat a device only through the test hook msm_test_sharded: its shards then run
+// one after another on that device.)
+int sharded_host(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                 const std::vector<int>& devs, Pt* r) {
+  const size_t D = devs.size();
+  std::vector<Pt> part(D, pt_identity());
+  int rc = for_each_device(D, [&](size_t i) {
+    size_t lo, hi;
+    shard_range(n, i, D, &lo, &hi);
+    const msm_opts od = opts_on(opts, devs[i]);
+    return host_entry(points_be + lo * 32, scalars_be + lo * 8, hi - lo, &od, &part[i]);
+  });
+  if (rc != MSM_OK) return rc;
+  *r = join_partials(part);
+  return MSM_OK;
+}
+
+int multi_host_entry(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts, Pt* r) {
+  if (!devices_listed(opts)) return host_entry(points_be, scalars_be, n, opts, r);
+  if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  std::vector<int> devs;
+  if (int rc = device_list(opts, &devs)) return rc;
+  return sharded_host(points_be, scalars_be, n, opts, devs, r);
+}
+
+// One shard of device-resident inputs that live on another device: copied over xGMI (a peer copy
+// on the slot's stream) into this device's wire buffers, then reduced here.
+int peer_shard(int owner, const uint32_t* d_points, const uint32_t* d_scalars, size_t cnt, const msm_opts* od,
+               Pt* r) {
+  return on_device(od, [&](DevCtx* c) -> int {
+    if (cnt == 0) {
+      *r = msmh::pt_identity();
+      return MSM_OK;
+    }
+    Slot& sl = c->slot[0];
+    Workspace& w = sl.ws;
+    int rc;
+    if ((rc = w.wire_pts.ensure(cnt * 128)) != MSM_OK || (rc = w.wire_sc.ensure(cnt * 32)) != MSM_OK) return rc;
+    HIPCHECK(hipMemcpyPeerAsync(w.wire_pts.p, c->device, d_points, owner, cnt * 128, sl.stream));
+    HIPCHECK(hipMemcpyPeerAsync(w.wire_sc.p, c->device, d_scalars, owner, cnt * 32, sl.stream));
+    rc = run_device(c, w.wire_pts.as<uint32_t>(), w.wire_sc.as<uint32_t>(), cnt, od, nullptr, r);
+    if (rc != MSM_OK) hipStreamSynchronize(sl.stream);  // the copies read the caller's buffers
+    return rc;
+  });
+}
+
+// msm_compute_device / msm_compute_device_partial: the inputs live on one listed device (the
+// owner), which reduces its shard in place; every other listed device copies its shard over.
+// (Through msm_test_sharded a device may be listed again: its later shards take the copy path.)
+int sharded_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                   void* hip_stream, const std::vector<int>& devs, Pt* r) {
+  int owner = devs[0];
+  if (n) {
+    hipPointerAttribute_t ap{}, as{};
+    if (hipPointerGetAttributes(&ap, d_points_be) != hipSuccess ||
+        hipPointerGetAttributes(&as, d_scalars_be) != hipSuccess) {
+      (void)hipGetLastError();
+      return MSM_ERR_INVALID_ARG;
+    }
+    owner = ap.device;
+    if (as.device != owner || std::find(devs.begin(), devs.end(), owner) == devs.end()) return MSM_ERR_INVALID_ARG;
+  }
+  if (hip_stream && n) {
+    // the peer copies start on other devices' streams: the inputs' producers finish first
+    DeviceGuard g(owner);
+    HIPCHECK(hipStreamSynchronize(hip_stream == MSM_STREAM_NULL ? nullptr : (hipStream_t)hip_stream));
+  }
+  const size_t D = devs.size();
+  const size_t own = (size_t)(std::find(devs.begin(), devs.end(), owner) - devs.begin());
+  std::vector<Pt> part(D, pt_identity());
+  int rc = for_each_device(D, [&](size_t i) {
+    size_t lo, hi;
+    shard_range(n, i, D, &lo, &hi);
+    const msm_opts od = opts_on(opts, devs[i]);
+    if (i == own)
+      return device_entry(d_points_be + lo * 32, d_scalars_be + lo * 8, hi - lo, &od, nullptr, &part[i]);
+    return peer_shard(owner, d_points_be + lo * 32, d_scalars_be + lo * 8, hi - lo, &od, &part[i]);
+  });
+  if (rc != MSM_OK) return rc;
+  *r = join_partials(part);
+  return MSM_OK;
+}
+
+int multi_device_entry(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, const msm_opts* opts,
+                       void* hip_stream, Pt* r) {
+  if (!devices_listed(opts)) return device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, r);
+  if ((!d_points_be || !d_scalars_be) && n) return MSM_ERR_INVALID_ARG;
+  std::vector<int> devs;
+  if (int rc = device_list(opts, &devs)) return rc;
+  return sharded_device(d_points_be, d_scalars_be, n, opts, hip_stream, devs, r);
+}
+
+// msm_compute_many / msm_compute_shared: a contiguous block of the MSMs per listed device
+// (whole MSMs, nothing to join).  Device batches take one device.
+int multi_many_entry(const ManyInputs& in, size_t n, size_t count, const msm_opts* opts, void* hip_stream,
+                     uint32_t* out, bool projective) {
+  if (!devices_listed(opts)) return many_entry(in, n, count, opts, hip_stream, out, projective);
+  if (in.kind != ManyInputs::HOST) return MSM_ERR_INVALID_ARG;
+  if (!out || (!in.scalars && count) || (!in.points && !in.shared_points && count)) return MSM_ERR_INVALID_ARG;
+  std::vector<int> devs;
+  if (int rc = device_list(opts, &devs)) return rc;
+  const size_t D = devs.size();
+  return for_each_device(D, [&](size_t i) -> int {
+    size_t b0, b1;
+    shard_range(count, i, D, &b0, &b1);
+    if (b0 == b1) return MSM_OK;
+    ManyInputs sub = in;
+    if (in.points) sub.points = in.points + b0;
+    sub.scalars = in.scalars + b0;
+    const msm_opts od = opts_on(opts, devs[i]);
+    return many_entry(sub, n, b1 - b0, &od, nullptr, out + b0 * (projective ? 32 : 16), projective);
+  });
+}
+
 }  // namespace
 
 extern "C" {
@@ -1446,6 +1631,12 @@ int msm_device_count(void) {
   return probe_devices();
 }
 
+int msm_device_ordinal(int index) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int n = probe_devices();
+  return index >= 0 && index < n ? g_gfx950[index] : -1;
+}
+
 const char* msm_strerror(int code) {
   switch (code) {
     case MSM_OK: return "ok";
@@ -1475,7 +1666,7 @@ int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n,
                 uint32_t out_xy_be[16]) {
   if (!out_xy_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = host_entry(points_be, scalars_be, n, opts, &r);
+  int rc = multi_host_entry(points_be, scalars_be, n, opts, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
@@ -1485,7 +1676,7 @@ int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, s
                         uint32_t out_xyzt_be[32]) {
   if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = host_entry(points_be, scalars_be, n, opts, &r);
+  int rc = multi_host_entry(points_be, scalars_be, n, opts, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_xyzt(r, out_xyzt_be);
   return MSM_OK;
@@ -1495,7 +1686,7 @@ int msm_compute_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be
                        void* hip_stream, uint32_t out_xy_be[16]) {
   if (!out_xy_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
+  int rc = multi_device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
@@ -1505,7 +1696,7 @@ int msm_compute_device_partial(const uint32_t* d_points_be, const uint32_t* d_sc
                                const msm_opts* opts, void* hip_stream, uint32_t out_xyzt_be[32]) {
   if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;
   Pt r;
-  int rc = device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
+  int rc = multi_device_entry(d_points_be, d_scalars_be, n, opts, hip_stream, &r);
   if (rc != MSM_OK) return rc;
   pt_to_be_xyzt(r, out_xyzt_be);
   return MSM_OK;
@@ -1516,7 +1707,7 @@ int msm_compute_many_device(const uint32_t* const* d_points_be, const uint32_t* 
   ManyInputs in;
   in.points = d_points_be;
   in.scalars = d_scalars_be;
-  return many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
+  return multi_many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
 }
 
 int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const uint32_t* const* d_scalars_be,
@@ -1525,7 +1716,7 @@ int msm_compute_many_device_partial(const uint32_t* const* d_points_be, const ui
   ManyInputs in;
   in.points = d_points_be;
   in.scalars = d_scalars_be;
-  return many_entry(in, n, count, opts, hip_stream, out_xyzt_be, true);
+  return multi_many_entry(in, n, count, opts, hip_stream, out_xyzt_be, true);
 }
 
 int msm_compute_batch_device(const uint32_t* d_points_be, const uint32_t* d_scalars_be, size_t n, size_t count,
@@ -1546,7 +1737,7 @@ int msm_compute_shared_device(const uint32_t* d_points_be, const uint32_t* const
   in.shared_points = d_points_be;
   in.scalars = d_scalars_be;
   if (!n) in.points = d_scalars_be;  // n = 0: identities, no input is read
-  return many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
+  return multi_many_entry(in, n, count, opts, hip_stream, out_xy_be, false);
 }
 
 int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
@@ -1555,7 +1746,7 @@ int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* sc
   in.kind = ManyInputs::HOST;
   in.points = points_be;
   in.scalars = scalars_be;
-  return many_entry(in, n, count, opts, nullptr, out_xy_be, false);
+  return multi_many_entry(in, n, count, opts, nullptr, out_xy_be, false);
 }
 
 int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
@@ -1566,7 +1757,7 @@ int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars
   in.shared_points = points_be;
   in.scalars = scalars_be;
   if (!n) in.points = scalars_be;
-  return many_entry(in, n, count, opts, nullptr, out_xy_be, false);
+  return multi_many_entry(in, n, count, opts, nullptr, out_xy_be, false);
 }
 
 int msm_combine_partials(const uint32_t* partials_xyzt_be, size_t count, uint32_t out_xy_be[16]) {
@@ -1660,11 +1851,11 @@ int msm_compute_cpu(const uint32_t* points_be, const uint32_t* scalars_be, size_
 
 int msm_set_profiling(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
-  g_profiling = enable < 0 ? 0 : enable > 2 ? 1 : enable;
+  g_profiling.store(enable < 0 ? 0 : enable > 2 ? 1 : enable);
   for (DevCtx* c : g_ctx)
     if (c) {
       std::lock_guard<std::mutex> lk2(c->mu);  // a call in flight on another thread finishes first
-      c->profiling = g_profiling;
+      c->profiling = g_profiling.load();
       c->last.accumulate_sum = c->last.device_total_sum = c->last.accumulate_union_sum = 0;
       c->last.profiled = 0;
     }
@@ -1697,7 +1888,33 @@ int msm_gen_scalars(uint64_t seed, size_t n, uint32_t* scalars_be) {
   return MSM_OK;
 }
 
-// ---- test hooks (not in msm.h): batch field / point ops on the device, canonical LE words ----
+// ---- test hooks (not in msm.h) ----
+// The device-list shard split (tests/test_host_logic.py checks it against msm_amd.dist).
+int msm_test_shard_range(size_t n, size_t i, size_t D, size_t* lo, size_t* hi) {
+  if (!lo || !hi || D == 0 || i >= D) return MSM_ERR_INVALID_ARG;
+  shard_range(n, i, D, lo, hi);
+  return MSM_OK;
+}
+
+// The sharded paths with a list that may repeat a device (the one-GPU box has no second device):
+// mode 0 = msm_compute (host inputs), 1 = msm_compute_device; affine result.
+int msm_test_sharded(int mode, const uint32_t* points, const uint32_t* scalars, size_t n, const msm_opts* opts,
+                     const int32_t* devices, uint32_t n_devices, void* hip_stream, uint32_t out_xy_be[16]) {
+  if (!opts || !devices || !n_devices || n_devices > MSM_MAX_DEVICES || !out_xy_be) return MSM_ERR_INVALID_ARG;
+  std::vector<int> devs(devices, devices + n_devices);
+  for (int d : devs) {
+    DevCtx* c;
+    if (int rc = get_ctx(d, &c)) return rc;
+  }
+  Pt r;
+  const int rc = mode == 0 ? sharded_host(points, scalars, n, opts, devs, &r)
+                           : sharded_device(points, scalars, n, opts, hip_stream, devs, &r);
+  if (rc != MSM_OK) return rc;
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
+// Batch field / point ops on the device, canonical LE words.
 int msm_test_field_op(uint32_t op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
   DevCtx* c;
   int rc = get_ctx(-1, &c);

@@ -3,14 +3,27 @@
 //
 // Exports (all compute is asynchronous through napi_async_work, resolving a Promise, because
 // compute_msm is async in the reference):
-//   computeMsmU32(points: Uint32Array(32n), scalars: Uint32Array(8n), windowSize) -> Promise<Uint32Array(16)>
-//   computeMsmBigInt(points: {x,y,t,z: bigint}[], scalars: bigint[], windowSize) -> Promise<Uint32Array(16)>
+//   computeMsmU32(points: Uint32Array(32n), scalars: Uint32Array(8n), windowSize, devices?)
+//       -> Promise<Uint32Array(16)>
+//   computeMsmBigInt(points: {x,y,t,z: bigint}[], scalars: bigint[], windowSize, devices?)
+//       -> Promise<Uint32Array(16)>
 //       BigInt -> big-endian u32 marshalling happens natively (napi_get_value_bigint_words),
 //       replacing convert_worker.ts:8-57 and the 8-worker fan-out of submission.ts:47-74.
+//   `devices` (an array of HIP ordinals) shards the MSM over those gfx950 devices in this one call
+//   (msm_opts MSM_FLAG_DEVICES: one host thread and PCIe link per device, partials joined with one
+//   EC add each -- the reference's CPU/GPU split of submission.ts:116-154 generalised).
+//
+// Input ownership while the promise is pending (the worker thread reads the inputs): typed arrays
+// over a SharedArrayBuffer -- what the reference's own compute_msm allocates
+// (submission.ts:35-39) and what submission.mjs's flattenU32 builds -- cannot be detached, so they
+// are read in place (a reference keeps them alive; writing them before the promise settles races
+// with the upload).  Typed arrays over a plain ArrayBuffer could be detached (transferred) by the
+// caller while the job runs, freeing the memory under the worker, so they are copied first.
 //   pointAddAffine(a: Uint32Array(16), b: Uint32Array(16)) -> Uint32Array(16)      (lib.rs:240-253)
 //   split(windowSize, scalars: Uint32Array(8n)) -> Uint32Array(W*n)                 (lib.rs:196-202)
 //   bestWindowSize(n) -> number                                                     (submission.ts:18-23)
-//   init() -> number (0 ok), deviceCount() -> number, strerror(code) -> string
+//   init() -> number (0 ok), deviceCount() -> number, deviceOrdinals() -> number[],
+//   strerror(code) -> string
 #include <node_api.h>
 
 #include <cstring>
@@ -32,14 +45,16 @@ namespace {
 struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
-  std::vector<uint32_t> points, scalars;  // marshalled BigInt inputs (computeMsmBigInt)
-  // computeMsmU32: the caller's typed arrays, held by references until the job completes and read
-  // in place by msm_compute (no staging copy; they must not be written while the promise is pending)
+  // marshalled BigInt inputs (computeMsmBigInt) or the copy of plain-ArrayBuffer typed arrays
+  std::vector<uint32_t> points, scalars;
+  // computeMsmU32 over SharedArrayBuffers: the caller's arrays, held by references until the job
+  // completes and read in place by msm_compute
   napi_ref ref_points = nullptr, ref_scalars = nullptr;
   const uint32_t* p_points = nullptr;
   const uint32_t* p_scalars = nullptr;
   size_t n = 0;
   uint32_t window = 0;
+  std::vector<int32_t> devices;  // empty: the current device
   uint32_t out[16] = {0};
   int rc = 0;
 };
@@ -50,6 +65,11 @@ void execute(napi_env, void* data) {
   memset(&o, 0, sizeof(o));
   o.window_bits = j->window;
   o.device = -1;
+  if (!j->devices.empty()) {
+    o.flags |= MSM_FLAG_DEVICES;
+    o.devices = j->devices.data();
+    o.n_devices = (uint32_t)j->devices.size();
+  }
   const uint32_t* pts = j->p_points ? j->p_points : j->points.data();
   const uint32_t* sc = j->p_scalars ? j->p_scalars : j->scalars.data();
   j->rc = msm_compute(pts, sc, j->n, &o, j->out);
@@ -88,7 +108,7 @@ napi_value start_job(napi_env env, Job* j) {
   return promise;
 }
 
-bool get_u32_array(napi_env env, napi_value v, const uint32_t** data, size_t* len) {
+bool get_u32_array(napi_env env, napi_value v, const uint32_t** data, size_t* len, bool* shared = nullptr) {
   bool is_ta = false;
   if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return false;
   napi_typedarray_type t;
@@ -97,7 +117,32 @@ bool get_u32_array(napi_env env, napi_value v, const uint32_t** data, size_t* le
   size_t off;
   if (napi_get_typedarray_info(env, v, &t, len, &d, &ab, &off) != napi_ok || t != napi_uint32_array) return false;
   *data = static_cast<const uint32_t*>(d);
+  if (shared) {  // napi_is_arraybuffer is false for a SharedArrayBuffer
+    bool plain = true;
+    if (napi_is_arraybuffer(env, ab, &plain) != napi_ok) return false;
+    *shared = !plain;
+  }
   return true;
+}
+
+// Optional device list: an array of HIP ordinals (undefined / null: none).  false on a bad value.
+bool get_devices(napi_env env, size_t argc, napi_value* argv, size_t at, std::vector<int32_t>* out) {
+  out->clear();
+  if (argc <= at) return true;
+  napi_valuetype vt;
+  if (napi_typeof(env, argv[at], &vt) != napi_ok) return false;
+  if (vt == napi_undefined || vt == napi_null) return true;
+  bool arr = false;
+  if (napi_is_array(env, argv[at], &arr) != napi_ok || !arr) return false;
+  uint32_t len = 0;
+  if (napi_get_array_length(env, argv[at], &len) != napi_ok) return false;
+  for (uint32_t i = 0; i < len; i++) {
+    napi_value e;
+    int32_t d;
+    if (napi_get_element(env, argv[at], i, &e) != napi_ok || napi_get_value_int32(env, e, &d) != napi_ok) return false;
+    out->push_back(d);
+  }
+  return true;  // shape and ordinals are checked by libmsm (msm_opts, MSM_ERR_INVALID_ARG)
 }
 
 uint32_t get_window(napi_env env, napi_value v) {
@@ -109,25 +154,35 @@ uint32_t get_window(napi_env env, napi_value v) {
 }
 
 napi_value ComputeMsmU32(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+  size_t argc = 4;
+  napi_value argv[4];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   const uint32_t *pts, *sc;
   size_t plen, slen;
-  if (argc < 2 || !get_u32_array(env, argv[0], &pts, &plen) || !get_u32_array(env, argv[1], &sc, &slen)) {
-    napi_throw_type_error(env, nullptr, "computeMsmU32(points: Uint32Array, scalars: Uint32Array, windowSize?)");
+  bool pshared = false, sshared = false;
+  std::vector<int32_t> devs;
+  if (argc < 2 || !get_u32_array(env, argv[0], &pts, &plen, &pshared) ||
+      !get_u32_array(env, argv[1], &sc, &slen, &sshared) || !get_devices(env, argc, argv, 3, &devs)) {
+    napi_throw_type_error(env, nullptr,
+                          "computeMsmU32(points: Uint32Array, scalars: Uint32Array, windowSize?, devices?: number[])");
     return nullptr;
   }
   Job* j = new Job();
   j->n = std::min(plen / 32, slen / 8);
-  j->p_points = pts;
-  j->p_scalars = sc;
-  if (napi_create_reference(env, argv[0], 1, &j->ref_points) != napi_ok ||
-      napi_create_reference(env, argv[1], 1, &j->ref_scalars) != napi_ok) {
-    if (j->ref_points) napi_delete_reference(env, j->ref_points);
-    delete j;
-    napi_throw_error(env, nullptr, "cannot reference the input arrays");
-    return nullptr;
+  j->devices = std::move(devs);
+  if (pshared && sshared) {
+    j->p_points = pts;
+    j->p_scalars = sc;
+    if (napi_create_reference(env, argv[0], 1, &j->ref_points) != napi_ok ||
+        napi_create_reference(env, argv[1], 1, &j->ref_scalars) != napi_ok) {
+      if (j->ref_points) napi_delete_reference(env, j->ref_points);
+      delete j;
+      napi_throw_error(env, nullptr, "cannot reference the input arrays");
+      return nullptr;
+    }
+  } else {  // detachable memory: the worker reads a copy
+    j->points.assign(pts, pts + j->n * 32);
+    j->scalars.assign(sc, sc + j->n * 8);
   }
   j->window = argc > 2 ? get_window(env, argv[2]) : 0;
   return start_job(env, j);
@@ -148,8 +203,8 @@ bool bigint_be(napi_env env, napi_value v, uint32_t* out8) {
 }
 
 napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+  size_t argc = 4;
+  napi_value argv[4];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   bool ap = false, as = false;
   if (argc < 2 || napi_is_array(env, argv[0], &ap) != napi_ok || !ap || napi_is_array(env, argv[1], &as) != napi_ok ||
@@ -161,6 +216,11 @@ napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
   NAPI_OK(napi_get_array_length(env, argv[0], &np_));
   NAPI_OK(napi_get_array_length(env, argv[1], &ns));
   Job* j = new Job();
+  if (!get_devices(env, argc, argv, 3, &j->devices)) {
+    delete j;
+    napi_throw_type_error(env, nullptr, "devices must be an array of device ordinals");
+    return nullptr;
+  }
   j->n = std::min(np_, ns);
   j->points.resize(j->n * 32);
   j->scalars.resize(j->n * 8);
@@ -264,6 +324,19 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
   return r;
 }
 
+// HIP ordinals of the gfx950 devices (the values a `devices` list takes).
+napi_value DeviceOrdinals(napi_env env, napi_callback_info) {
+  napi_value arr;
+  const int n = msm_device_count();
+  NAPI_OK(napi_create_array_with_length(env, n > 0 ? n : 0, &arr));
+  for (int i = 0; i < n; i++) {
+    napi_value v;
+    NAPI_OK(napi_create_int32(env, msm_device_ordinal(i), &v));
+    NAPI_OK(napi_set_element(env, arr, i, v));
+  }
+  return arr;
+}
+
 napi_value StrError(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -284,6 +357,7 @@ napi_value ModuleInit(napi_env env, napi_value exports) {
       {"bestWindowSize", nullptr, BestWindowSize, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"init", nullptr, Init, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"deviceOrdinals", nullptr, DeviceOrdinals, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"strerror", nullptr, StrError, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);

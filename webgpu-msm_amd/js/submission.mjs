@@ -5,13 +5,19 @@
 //   compute_msm(baseAffinePoints: BigIntPoint[] | U32ArrayPoint[],
 //               scalars: bigint[] | Uint32Array[]) => Promise<{ x: bigint, y: bigint }>
 //
-// Also accepted (an extension): flat wire buffers, a Uint32Array of n x 32 point words and one of
-// n x 8 scalar words -- the layout flattenU32 builds -- which skips the JS marshalling.
+// Also accepted (an extension, and the fast form): flat wire buffers, a Uint32Array of n x 32
+// point words and one of n x 8 scalar words -- the layout flattenU32 builds -- which skips the JS
+// marshalling of n point objects (at 2^20 that marshalling is ~25x the MSM itself).  Flat arrays
+// over a SharedArrayBuffer (as the reference allocates them, submission.ts:35-39) are read in
+// place; over a plain ArrayBuffer the addon copies them first (they could be detached meanwhile).
 //
 // The browser-only knobs (?windowSize=, submission.ts:29-33) become an optional third
-// argument { windowSize } or the MSM_WINDOW_SIZE environment variable.  { cpuWorkRatio }
-// (?cpuWorkRatio, submission.ts:96-154) is accepted and the whole MSM runs on the GPU: the host
-// would take ~1000x longer for its share, and the result is the same.
+// argument { windowSize } or the MSM_WINDOW_SIZE environment variable.  { devices: [0, 1, ...] }
+// shards the MSM over those gfx950 devices inside this one call (one host thread and PCIe link
+// each, partials joined with one EC add each) -- the multi-device form of the reference's
+// CPU/GPU split (?cpuWorkRatio, submission.ts:96-154).  { cpuWorkRatio } itself is accepted and
+// the whole MSM runs on the GPU(s): the host would take ~1000x longer for its share, and the
+// result is the same.
 // There is no WebGPU/WGSL/CPU fallback: without the addon or a gfx950 device this rejects.
 import { createRequire } from "module";
 import fs from "fs";
@@ -48,10 +54,12 @@ export function u32ArrayToBigInts(u32Array) {
 // Element-wise copies: on Node 12 a per-coordinate TypedArray.set() costs more than the 8 word
 // copies it replaces (2^20 points: ~15-30% faster flatten, measured locally).
 // Exported for tools/node_e2e.mjs, which times this JS marshalling share of compute_msm.
+// The buffers live on SharedArrayBuffers (as in submission.ts:35-39), so the addon reads them in
+// place.
 export function flattenU32(points, scalars) {
   const n = Math.min(points.length, scalars.length);
-  const pb = new Uint32Array(n * nUint32PerPoint);
-  const sb = new Uint32Array(n * nUint32PerScalar);
+  const pb = new Uint32Array(new SharedArrayBuffer(n * nUint32PerPoint * 4));
+  const sb = new Uint32Array(new SharedArrayBuffer(n * nUint32PerScalar * 4));
   for (let i = 0; i < n; i++) {
     const p = points[i];
     const o = i * 32;
@@ -71,13 +79,20 @@ export function flattenU32(points, scalars) {
   return [pb, sb];
 }
 
+function devicesFrom(options) {
+  if (!options || options.devices === undefined || options.devices === null) return undefined;
+  if (!Array.isArray(options.devices)) throw new TypeError("options.devices must be an array of device ordinals");
+  return options.devices;
+}
+
 export const compute_msm = async (baseAffinePoints, scalars, options) => {
   const windowSize = windowFrom(options);
+  const devices = devicesFrom(options);
   if (baseAffinePoints instanceof Uint32Array && scalars instanceof Uint32Array) {
     // already flat wire buffers (x|y|t|z BE words per point, BE words per scalar): no marshalling
     const n = Math.min(Math.floor(baseAffinePoints.length / nUint32PerPoint), Math.floor(scalars.length / nUint32PerScalar));
     const result = await addon.computeMsmU32(baseAffinePoints.subarray(0, n * nUint32PerPoint),
-                                             scalars.subarray(0, n * nUint32PerScalar), windowSize);
+                                             scalars.subarray(0, n * nUint32PerScalar), windowSize, devices);
     const [x, y] = u32ArrayToBigInts(result);
     return { x, y };
   }
@@ -89,10 +104,10 @@ export const compute_msm = async (baseAffinePoints, scalars, options) => {
     // native marshalling (napi_get_value_bigint_words) replaces convert_worker.ts
     const pts = typeof baseAffinePoints[0].x === "bigint" ? baseAffinePoints : baseAffinePoints.map(toBigIntPoint);
     const sc = typeof scalars[0] === "bigint" ? scalars : scalars.map((s) => u32ArrayToBigInts(s)[0]);
-    result = await addon.computeMsmBigInt(pts, sc, windowSize);
+    result = await addon.computeMsmBigInt(pts, sc, windowSize, devices);
   } else {
     const [pointBuffer, scalarBuffer] = flattenU32(baseAffinePoints, scalars);
-    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize);
+    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize, devices);
   }
   const [x, y] = u32ArrayToBigInts(result);
   return { x, y };
@@ -112,6 +127,7 @@ export const split_dynamic = (windowSize, scalarsU32) => addon.split(windowSize,
 export const point_add_affine = (a16, b16) => addon.pointAddAffine(a16, b16);
 export const init = () => addon.init();
 export const deviceCount = () => addon.deviceCount();
+export const deviceOrdinals = () => addon.deviceOrdinals();
 
 // loadTestCase (src/test-data/testCases.ts:34-52): JSON-lines points whose string fields are
 // BigInts, and one decimal scalar per line.  Paths instead of fetch() URLs (Node, not a browser).

@@ -23,7 +23,8 @@ __all__ = [
     "compute_msm_partial", "compute_msm_device_partial", "compute_msm_many_device", "compute_msm_many_device_partial",
     "compute_msm_shared_device", "compute_msm_many", "compute_msm_shared", "compute_msm_cpu", "MSM_FLAG_SERIAL",
     "combine_partials", "combine_partials_many", "point_add_affine",
-    "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count",
+    "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count", "device_ordinals",
+    "MSM_FLAG_DEVICES", "MSM_MAX_DEVICES",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
 
@@ -42,8 +43,12 @@ class MsmError(RuntimeError):
 
 
 class MsmOpts(ctypes.Structure):
+    """include/msm.h msm_opts: the original four fields, then the device list (read by libmsm only
+    when flags has MSM_FLAG_DEVICES)."""
     _fields_ = [("window_bits", ctypes.c_uint32), ("run_length", ctypes.c_uint32),
-                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("devices", ctypes.POINTER(ctypes.c_int32)), ("n_devices", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class MsmProfile(ctypes.Structure):
@@ -56,6 +61,8 @@ class MsmProfile(ctypes.Structure):
         ("msms_per_launch", ctypes.c_uint32), ("accumulate_union_sum", ctypes.c_double)]
 
 MSM_FLAG_SERIAL = 1  # pipelined entries: one launch in flight at a time
+MSM_FLAG_DEVICES = 2  # msm_opts carries a device list (include/msm.h)
+MSM_MAX_DEVICES = 16
 MSM_STREAM_NULL = 1  # hip_stream value: order after the null (legacy default) stream
 
 
@@ -90,6 +97,7 @@ def load() -> ctypes.CDLL:
         "msm_init": ([], ctypes.c_int),
         "msm_shutdown": ([], None),
         "msm_device_count": ([], ctypes.c_int),
+        "msm_device_ordinal": ([ctypes.c_int], ctypes.c_int),
         "msm_strerror": ([ctypes.c_int], ctypes.c_char_p),
         "msm_best_window": ([sz], ctypes.c_uint32),
         "msm_compute": ([vp, vp, sz, optp, u32p], ctypes.c_int),
@@ -114,6 +122,9 @@ def load() -> ctypes.CDLL:
         "msm_last_profile": ([ctypes.POINTER(MsmProfile)], ctypes.c_int),
         "msm_test_field_op": ([ctypes.c_uint32, vp, vp, u32p, sz], ctypes.c_int),
         "msm_test_point_op": ([ctypes.c_uint32, vp, vp, u32p, sz], ctypes.c_int),
+        "msm_test_shard_range": ([sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)], ctypes.c_int),
+        "msm_test_sharded": ([ctypes.c_int, vp, vp, sz, optp, ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, vp,
+                              u32p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -148,8 +159,18 @@ def _out(n: int) -> Tuple[np.ndarray, ctypes.POINTER(ctypes.c_uint32)]:
     return o, o.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
 
 
-def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1, flags: int = 0):
-    return ctypes.byref(MsmOpts(int(window_size or 0), int(run_length or 0), int(device), int(flags)))
+def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1, flags: int = 0,
+          devices: Optional[Sequence[int]] = None):
+    """A msm_opts by reference.  `devices` (a list of HIP ordinals) runs the call on several
+    devices (MSM_FLAG_DEVICES); the array is kept alive by the returned object."""
+    o = MsmOpts(int(window_size or 0), int(run_length or 0), int(device), int(flags))
+    if devices is not None:
+        arr = (ctypes.c_int32 * max(len(devices), 1))(*[int(d) for d in devices])
+        o.devices = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
+        o.n_devices = len(devices)
+        o.flags |= MSM_FLAG_DEVICES
+        o._keep = arr
+    return ctypes.byref(o)
 
 
 def wire_to_int(words: Iterable[int]) -> int:
@@ -218,33 +239,38 @@ def get_best_window_size(n: int) -> int:
 
 
 def compute_msm_wire(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
-                     run_length: Optional[int] = None, device: int = -1) -> Tuple[int, int]:
+                     run_length: Optional[int] = None, device: int = -1,
+                     devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+    """msm_compute on host wire arrays; `devices` shards the points over those HIP ordinals."""
     L = load()
     pts = _u32(points_wire).reshape(-1, 32)
     sc = _u32(scalars_wire).reshape(-1, 8)
     n = min(pts.shape[0], sc.shape[0])  # the oracle zips to the shorter length
     pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
     o, op = _out(16)
-    _check(L.msm_compute(_ptr(pts), _ptr(sc), n, _opts(window_size, run_length, device), op), "msm_compute")
+    _check(L.msm_compute(_ptr(pts), _ptr(sc), n, _opts(window_size, run_length, device, devices=devices), op),
+           "msm_compute")
     return _xy(o)
 
 
 def compute_msm(base_affine_points, scalars, window_size: Optional[int] = None,
-                run_length: Optional[int] = None, device: int = -1) -> Tuple[int, int]:
+                run_length: Optional[int] = None, device: int = -1,
+                devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
     """compute_msm (submission.ts:25-157): MSM of BigIntPoint[]/U32ArrayPoint[] with bigint[]/Uint32Array[]."""
     return compute_msm_wire(points_to_wire(base_affine_points), scalars_to_wire(scalars), window_size,
-                            run_length, device)
+                            run_length, device, devices)
 
 
 def compute_msm_partial(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
-                        device: int = -1) -> np.ndarray:
+                        device: int = -1, devices: Optional[Sequence[int]] = None) -> np.ndarray:
     L = load()
     pts = _u32(points_wire).reshape(-1, 32)
     sc = _u32(scalars_wire).reshape(-1, 8)
     n = min(pts.shape[0], sc.shape[0])
     pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
     o, op = _out(32)
-    _check(L.msm_compute_partial(_ptr(pts), _ptr(sc), n, _opts(window_size, None, device), op), "msm_compute_partial")
+    _check(L.msm_compute_partial(_ptr(pts), _ptr(sc), n, _opts(window_size, None, device, devices=devices), op),
+           "msm_compute_partial")
     return o
 
 
@@ -272,20 +298,25 @@ def _first(xs):
 
 
 def compute_msm_device(d_points, d_scalars, n: int, window_size: Optional[int] = None,
-                       run_length: Optional[int] = None, device: int = -1, stream: int = 0) -> Tuple[int, int]:
-    """Inputs already in HBM (torch tensors or raw device pointers, wire layout)."""
+                       run_length: Optional[int] = None, device: int = -1, stream: int = 0,
+                       devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+    """Inputs already in HBM (torch tensors or raw device pointers, wire layout).  With `devices`
+    the listed devices other than the inputs' own copy their shard over xGMI and reduce it."""
     L = load()
     o, op = _out(16)
-    _check(L.msm_compute_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, run_length, device),
+    _check(L.msm_compute_device(_dev_ptr(d_points), _dev_ptr(d_scalars), n,
+                                _opts(window_size, run_length, device, devices=devices),
                                 _stream(stream, d_points, d_scalars), op), "msm_compute_device")
     return _xy(o)
 
 
 def compute_msm_device_partial(d_points, d_scalars, n: int, window_size: Optional[int] = None,
-                               device: int = -1, stream: int = 0) -> np.ndarray:
+                               device: int = -1, stream: int = 0,
+                               devices: Optional[Sequence[int]] = None) -> np.ndarray:
     L = load()
     o, op = _out(32)
-    _check(L.msm_compute_device_partial(_dev_ptr(d_points), _dev_ptr(d_scalars), n, _opts(window_size, None, device),
+    _check(L.msm_compute_device_partial(_dev_ptr(d_points), _dev_ptr(d_scalars), n,
+                                        _opts(window_size, None, device, devices=devices),
                                         _stream(stream, d_points, d_scalars), op), "msm_compute_device_partial")
     return o
 
@@ -343,7 +374,8 @@ def _host_list(arrs, words: int):
 
 
 def compute_msm_many(points_list, scalars_list, n: int, window_size: Optional[int] = None,
-                     run_length: Optional[int] = None, device: int = -1, flags: int = 0) -> np.ndarray:
+                     run_length: Optional[int] = None, device: int = -1, flags: int = 0,
+                     devices: Optional[Sequence[int]] = None) -> np.ndarray:
     """len(points_list) independent n-point MSMs of HOST arrays (wire [n, 32] / [n, 8] each),
     uploaded into libmsm's in-flight launch slots while the others compute.  [count][16]."""
     L = load()
@@ -357,12 +389,13 @@ def compute_msm_many(points_list, scalars_list, n: int, window_size: Optional[in
             raise ValueError("an input holds fewer than n points/scalars")
     o, op = _out(16 * max(count, 1))
     _check(L.msm_compute_many(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n, count,
-                              _opts(window_size, run_length, device, flags), op), "msm_compute_many")
+                              _opts(window_size, run_length, device, flags, devices), op), "msm_compute_many")
     return o[:16 * count].reshape(count, 16)
 
 
 def compute_msm_shared(points_wire, scalars_list, n: Optional[int] = None, window_size: Optional[int] = None,
-                       run_length: Optional[int] = None, device: int = -1, flags: int = 0) -> np.ndarray:
+                       run_length: Optional[int] = None, device: int = -1, flags: int = 0,
+                       devices: Optional[Sequence[int]] = None) -> np.ndarray:
     """Prover batch of HOST arrays: one base vector [n, 32], len(scalars_list) scalar vectors
     [n, 8]; the base vector is uploaded and prepared once.  [count][16]."""
     L = load()
@@ -374,7 +407,7 @@ def compute_msm_shared(points_wire, scalars_list, n: Optional[int] = None, windo
     count = len(ks)
     o, op = _out(16 * max(count, 1))
     _check(L.msm_compute_shared(_ptr(pts), ctypes.cast(ss, ctypes.c_void_p), n, count,
-                                _opts(window_size, run_length, device, flags), op), "msm_compute_shared")
+                                _opts(window_size, run_length, device, flags, devices), op), "msm_compute_shared")
     return o[:16 * count].reshape(count, 16)
 
 
@@ -488,6 +521,12 @@ def device_count() -> int:
     return int(load().msm_device_count())
 
 
+def device_ordinals() -> list:
+    """HIP ordinals of the visible gfx950 devices (msm_device_ordinal)."""
+    L = load()
+    return [int(L.msm_device_ordinal(i)) for i in range(int(L.msm_device_count()))]
+
+
 def _test_field_op(op: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Device field op on canonical little-endian word arrays [n, 8] (test hook)."""
     L = load()
@@ -506,3 +545,20 @@ def _test_point_op(op: int, p: np.ndarray, q: np.ndarray) -> np.ndarray:
     o, op_ = _out(p.shape[0] * 32)
     _check(L.msm_test_point_op(op, _ptr(p), _ptr(q), op_, p.shape[0]), "msm_test_point_op")
     return o.reshape(-1, 32)
+
+
+def _test_sharded(mode: int, points, scalars, n: int, devices: Sequence[int], window_size: Optional[int] = None,
+                  stream: int = 0) -> Tuple[int, int]:
+    """Test hook: the device-list shard/join paths with a list that may repeat a device (mode 0:
+    host wire arrays as msm_compute, 1: device-resident inputs as msm_compute_device)."""
+    L = load()
+    arr = (ctypes.c_int32 * len(devices))(*devices)
+    o, op = _out(16)
+    if mode == 0:
+        pts = np.ascontiguousarray(_u32(points).reshape(-1, 32)[:n])
+        sc = np.ascontiguousarray(_u32(scalars).reshape(-1, 8)[:n])
+        pp, sp, st = _ptr(pts), _ptr(sc), None
+    else:
+        pp, sp, st = _dev_ptr(points), _dev_ptr(scalars), _stream(stream, points, scalars)
+    _check(L.msm_test_sharded(mode, pp, sp, n, _opts(window_size), arr, len(devices), st, op), "msm_test_sharded")
+    return _xy(o)
