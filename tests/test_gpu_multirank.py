@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _torchrun(nproc, *bench_args, timeout=240):
-    env = dict(os.environ, MSM_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    env = dict(os.environ, MSM_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 2000),
            os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), *bench_args]
@@ -49,4 +49,21 @@ def test_prover_batch_replicas_2_ranks():
     # configs[4] code path: 16 distinct-seed 2^18-point MSMs over one base vector, dealt to 2 ranks
     out = _torchrun(2, "--batch", "16", "--points", str(1 << 18), "--steps", "2", "--warmup", "1")
     assert out["results_checked"] == 32
+    assert out["correct"] is True
+
+
+def test_point_sharded_8_ranks_configs3_shape():
+    # configs[3] at its real shape: 8 ranks, 2^17-point shards (the throughput window and four
+    # MSMs per launch), the 8-way batched join on rank 0
+    out = _torchrun(8, "--points", str(1 << 20), "--steps", "4", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
+                    timeout=420)
+    assert out["n_gpus"] == 8 and out["results_checked"] == 4
+    assert out["correct"] is True
+
+
+def test_prover_batch_64_replicas_configs4_shape():
+    # configs[4] at its real shape: 64 distinct-seed 2^18-point MSMs over one base vector, dealt
+    # to 2 ranks; every one of the 64 results checked against its closed form
+    out = _torchrun(2, "--batch", "64", "--points", str(1 << 18), "--steps", "1", "--warmup", "1", timeout=300)
+    assert out["results_checked"] == 64
     assert out["correct"] is True

@@ -19,6 +19,7 @@
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
+#   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
 [ $# -ge 2 ] || { sed -n 2,24p "$0"; exit 2; }
@@ -43,14 +44,14 @@ run() {  # name timeout cmd...
   fi
 }
 
-pytest_gpu() { python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread "$@"; }
+PYTEST=(python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread)
 
 for step in "$@"; do
   case $step in
-    tests) run tests 900 pytest_gpu ;;
+    tests) run tests 900 "${PYTEST[@]}" ;;
     tests_alt)
-      MSM_NO_GRAPH=1 run tests_eager 900 pytest_gpu -k "not random_sweep"
-      MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 pytest_gpu -k "not random_sweep" ;;
+      MSM_NO_GRAPH=1 run tests_eager 900 "${PYTEST[@]}" -k "not random_sweep"
+      MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 "${PYTEST[@]}" -k "not random_sweep" ;;
     bench) run bench 300 python bench.py ;;
     bench50) run bench50 300 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" ;;
     sizes)
@@ -76,6 +77,16 @@ for step in "$@"; do
       for r in $(seq 1 "${rounds:-3}"); do
         for lib in ${libs//,/ }; do
           MSM_AMD_LIB=$LIBDIR/$lib run "ab_${lib%.so}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+        done
+      done ;;
+    env:*)
+      IFS=: read -r _ spec rounds <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for r in $(seq 1 "${rounds:-3}"); do
+        for v in ${vals//,/ }; do
+          env "$var=$v" bash -c 'true' && export "$var=$v"
+          run "env_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          unset "$var"
         done
       done ;;
     ubench)

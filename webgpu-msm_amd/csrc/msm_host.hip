@@ -187,6 +187,10 @@ constexpr int NSEG = 6;
 // others' kernels) and while the host finishes launch j (window Horner).
 struct Slot {
   hipStream_t stream = nullptr;
+  // k_prepare_points forks onto aux (ev_fork) and rejoins before the accumulation (ev_join): the
+  // point preparation (HBM streaming) runs beside the bucket sort (the scalars' kernels)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Workspace ws;
   HostBuf h_out;  // k_bucket_reduce_2 writes the window terms, err and total here
   void* h_out_dev = nullptr;
@@ -262,7 +266,9 @@ int get_ctx(int device, DevCtx** out) {
       return MSM_ERR_HIP;
     }
     bool ok = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
-    for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
+    for (Slot& sl : c->slot)
+      ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess &&
+           hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
       delete c;
       hipSetDevice(prev);
@@ -280,6 +286,8 @@ int get_ctx(int device, DevCtx** out) {
       hipEventCreate(&sl.ev_end);
       hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming);
+      hipEventCreateWithFlags(&sl.ev_fork, hipEventDisableTiming);
+      hipEventCreateWithFlags(&sl.ev_join, hipEventDisableTiming);
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -453,6 +461,13 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
 
 inline unsigned grid_for(size_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
+// Whether a launch sequence holding both the point preparation and the sort runs the two side by
+// side (MSM_FORK_PREP=0 keeps them in order on one stream, for A/B runs).
+bool fork_prepare() {
+  static const bool on = !(getenv("MSM_FORK_PREP") && atoi(getenv("MSM_FORK_PREP")) == 0);
+  return on;
+}
+
 // Whether k_prepare_points writes `records` point records with nontemporal stores: only when they
 // outgrow the Infinity Cache (>= 128 MiB, i.e. 2^20 records; MSM_PP_NT=0/1 forces it).
 uint32_t prep_nt(size_t records) {
@@ -486,10 +501,22 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   };
   const uint32_t* total = w.bin_base.as<uint32_t>() + d.nbins;
   const unsigned rgrid = grid_for(pl.runs_max, ACC_THREADS);
+  // The preparation reads only the points and the sort only the scalars: with both in this
+  // sequence the preparation forks onto the slot's aux stream (a parallel branch of the captured
+  // graph) and rejoins before the accumulation, so a lone MSM's sort no longer waits behind it.
+  // (Profiling mode 1 keeps them in order, one event between every phase.)
+  const bool fork = (parts & PART_PREP) && (parts & PART_SORT) && !prof && fork_prepare();
   if (parts & PART_PREP) {
     mark(PH_START);
-    hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, s,
+    hipStream_t ps = s;
+    if (fork) {
+      HIPCHECK(hipEventRecord(sl.ev_fork, s));
+      HIPCHECK(hipStreamWaitEvent(sl.aux, sl.ev_fork, 0));
+      ps = sl.aux;
+    }
+    hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, ps,
                        d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n));
+    if (fork) HIPCHECK(hipEventRecord(sl.ev_join, sl.aux));
     mark(PH_PREPARE);
   }
   if (parts & PART_SORT) {
@@ -530,6 +557,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                        w.cursor.as<uint32_t>(), w.sorted_entry.as<uint32_t>());
     mark(PH_FINE);
   }
+  if (fork) HIPCHECK(hipStreamWaitEvent(s, sl.ev_join, 0));
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
   if (parts & PART_ACC) {
     hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
@@ -1608,7 +1636,7 @@ void msm_shutdown(void) {
       for (Segment& sg : sl.seg) sg.drop();
       sl.h_out.release();
       sl.h_out_dev = nullptr;
-      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in})
+      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in, sl.ev_fork, sl.ev_join})
         if (e) hipEventDestroy(e);
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
@@ -1616,7 +1644,10 @@ void msm_shutdown(void) {
     hipEventDestroy(c->ev_user);
     hipEventDestroy(c->ev_shared);
     hipEventDestroy(c->ev_base);
-    for (Slot& sl : c->slot) hipStreamDestroy(sl.stream);
+    for (Slot& sl : c->slot) {
+      hipStreamDestroy(sl.stream);
+      hipStreamDestroy(sl.aux);
+    }
     hipStreamDestroy(c->copy_stream);
     hipSetDevice(prev);
   }
