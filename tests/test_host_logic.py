@@ -184,3 +184,36 @@ def test_device_shard_join_equals_whole_msm():
             for j, v in enumerate((x, y, x * y % O.P, 1)):
                 parts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
         assert M.combine_partials(parts) == whole
+
+
+def _host_mont_words(v):
+    m = v * (1 << 256) % O.P  # the host's Montgomery form (hostfield.h, R = 2^256), LE words
+    return [(m >> (32 * q)) & 0xFFFFFFFF for q in range(8)]
+
+
+@pytest.mark.parametrize("n", [1 << 12, 1 << 20])
+def test_lone_msm_tail_threads_agree(n):
+    """The window-parallel tail of a lone MSM (TailCrew: helper threads sum each window's terms,
+    the caller runs the outer Horner) equals the one-thread Horner (which every GPU parity test
+    checks end to end), identity terms included."""
+    L = M.load()
+    words = L.msm_test_tail_words(n)
+    rng = np.random.default_rng(n)
+    terms = np.zeros(words, np.uint32)
+    pts = []
+    for i in range(words // 32):
+        if i % 7 == 3:  # an identity term (X = 0, Y = Z)
+            x, y, z = 0, 1, 5
+        else:
+            x, y = O.scalar_mul(O.G, int(rng.integers(1, 1 << 40)))
+            z = int(rng.integers(1, 1 << 40))
+        pts.append((x, y))
+        for j, v in enumerate((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)):
+            terms[i * 32 + 8 * j: i * 32 + 8 * j + 8] = _host_mont_words(v)
+    got = {}
+    for helpers in (0, 1, 3):
+        out = (ctypes.c_uint32 * 16)()
+        ms = ctypes.c_double()
+        assert L.msm_test_tail(n, terms.ctypes.data, helpers, out, ctypes.byref(ms)) == 0
+        got[helpers] = (M.wire_to_int(out[:8]), M.wire_to_int(out[8:]))
+    assert got[0] == got[1] == got[3]

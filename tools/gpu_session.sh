@@ -20,6 +20,7 @@
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
 #   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
+#   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
 [ $# -ge 2 ] || { sed -n 2,24p "$0"; exit 2; }
@@ -84,8 +85,18 @@ for step in "$@"; do
       var=${spec%%=*}; vals=${spec#*=}
       for r in $(seq 1 "${rounds:-3}"); do
         for v in ${vals//,/ }; do
-          env "$var=$v" bash -c 'true' && export "$var=$v"
+          export "$var=$v"
           run "env_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          unset "$var"
+        done
+      done ;;
+    lat:*)
+      IFS=: read -r _ spec rounds <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for r in $(seq 1 "${rounds:-3}"); do
+        for v in ${vals//,/ }; do
+          export "$var=$v"
+          run "lat_${var}_${v}_$r" 120 python tools/latency_probe.py
           unset "$var"
         done
       done ;;

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -604,52 +605,147 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
 // positions).  Follows reduce_last (lib.rs:88-104) in role: doublings between windows, then
 // into_affine.  The device already emitted the terms in this file's Montgomery form
 // (fe_to_host_mont).  Runs of doublings skip T (pt_dbl_proj) except the one feeding an add.
-Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
+
+Pt term_at(const uint32_t* o) {
+  Pt p;
+  memcpy(p.X.l, o, 32);
+  memcpy(p.Y.l, o + 8, 32);
+  memcpy(p.T.l, o + 16, 32);
+  memcpy(p.Z.l, o + 24, 32);
+  return p;
+}
+
+// (bit position - base, term) pairs of windows [w0, w1) of MSM terms block `terms`: V slices at
+// the window's offset, R_k once per set bit b of L at offset + k + b; identity terms skipped.
+void collect_terms(const Plan& pl, const uint32_t* terms, uint32_t w0, uint32_t w1, uint32_t base,
+                   std::vector<std::pair<uint32_t, const uint32_t*>>* at) {
   const MsmDims& d = pl.d;
-  terms += (size_t)m * d.Wm * pl.nterms * 32;  // MSM m's windows
-  // (bit position, term) pairs in descending position: V slices at the window's offset, R_k once
-  // per set bit b of L at offset + k + b
-  std::vector<std::pair<uint32_t, uint32_t>> at;
-  at.reserve((size_t)d.Wm * pl.nterms * 2);
-  for (uint32_t w = 0; w < d.Wm; w++)
+  for (uint32_t w = w0; w < w1; w++)
     for (uint32_t t = 0; t < pl.nterms; t++) {
-      const uint32_t i = w * pl.nterms + t;
-      const uint32_t* o = terms + (size_t)i * 32;
+      const uint32_t* o = terms + (size_t)(w * pl.nterms + t) * 32;
       Fq X;
       memcpy(X.l, o, 32);
       if (fq_is_zero(X) && !memcmp(o + 8, o + 24, 32)) continue;  // identity: X = 0, Y = Z
-      const uint32_t off = win_off(d, w);
+      const uint32_t off = win_off(d, w) - base;
       if (t < pl.nv) {
-        at.emplace_back(off, i);
+        at->emplace_back(off, o);
       } else {
         for (uint32_t b = 0; (pl.L >> b) != 0; b++)
-          if ((pl.L >> b) & 1u) at.emplace_back(off + (t - pl.nv) + b, i);
+          if ((pl.L >> b) & 1u) at->emplace_back(off + (t - pl.nv) + b, o);
       }
     }
+}
+
+// sum_j 2^(pos_j) P_j by Horner in descending position; get(j) gives P_j.
+template <typename Get>
+Pt horner_run(std::vector<std::pair<uint32_t, const uint32_t*>>& at, Get&& get) {
   std::stable_sort(at.begin(), at.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-  std::vector<uint32_t> pos(at.size()), idx(at.size());
-  for (size_t j = 0; j < at.size(); j++) {
-    pos[j] = at[j].first;
-    idx[j] = at[j].second;
-  }
   Pt acc = pt_identity();
-  if (pos.empty()) return acc;
-  for (size_t j = 0; j < pos.size(); j++) {
-    const uint32_t* o = terms + (size_t)idx[j] * 32;
-    Pt p;
-    memcpy(p.X.l, o, 32);
-    memcpy(p.Y.l, o + 8, 32);
-    memcpy(p.T.l, o + 16, 32);
-    memcpy(p.Z.l, o + 24, 32);
+  for (size_t j = 0; j < at.size(); j++) {
+    const Pt p = get(at[j].second);
     // T of the sum is needed when another add follows at the same position, and for the final
     // result (msm_compute_partial returns X|Y|T|Z); a doubling next never reads it
-    const bool want_t = j + 1 == pos.size() || pos[j + 1] == pos[j];
+    const bool want_t = j + 1 == at.size() || at[j + 1].first == at[j].first;
     acc = j == 0 ? p : pt_add(acc, p, want_t);
-    const uint32_t next = j + 1 < pos.size() ? pos[j + 1] : 0u;
-    if (pos[j] > next) acc = pt_dbl_n(acc, (int)(pos[j] - next));
+    const uint32_t next = j + 1 < at.size() ? at[j + 1].first : 0u;
+    if (at[j].first > next) acc = pt_dbl_n(acc, (int)(at[j].first - next));
   }
   return acc;
 }
+
+Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
+  const MsmDims& d = pl.d;
+  terms += (size_t)m * d.Wm * pl.nterms * 32;  // MSM m's windows
+  std::vector<std::pair<uint32_t, const uint32_t*>> at;
+  at.reserve((size_t)d.Wm * pl.nterms * 2);
+  collect_terms(pl, terms, 0, d.Wm, 0, &at);
+  return horner_run(at, term_at);
+}
+
+// The tail of a lone MSM (its latency, not a pipeline's throughput, is what counts), spread over
+// helper threads started BEFORE the device finishes (so no thread start-up sits on the critical
+// path; they spin until the terms land).  The helpers compute the window sums
+// W_w = sum 2^(pos - off_w) term top window first, while the calling thread runs the outer Horner
+// MSM = sum_w 2^(off_w) W_w, taking each W_w as it becomes ready: ~254 doublings and ~W adds on the
+// critical path instead of ~254 doublings and ~W * nterms adds.  MSM_TAIL_THREADS sets the helper
+// count (default 3; 0 = the one-thread horner_tail).
+int tail_helpers() {
+  static const int v = getenv("MSM_TAIL_THREADS") ? std::max(0, std::min(16, atoi(getenv("MSM_TAIL_THREADS")))) : 3;
+  return v;
+}
+
+class TailCrew {
+ public:
+  explicit TailCrew(int helpers) {
+    for (int i = 0; i < helpers; i++) th_.emplace_back([this] { work(); });
+  }
+  ~TailCrew() {
+    quit_.store(true);
+    for (std::thread& t : th_) t.join();
+  }
+  bool active() const { return !th_.empty(); }
+  // The terms are on the host: the helpers start on the window sums, the caller on the outer
+  // Horner.
+  Pt run(const Plan& pl, const uint32_t* terms) {
+    pl_ = &pl;
+    terms_ = terms;
+    const uint32_t Wm = pl.d.Wm;
+    sums_.assign(Wm, pt_identity());
+    ready_.reset(new std::atomic<int>[Wm]);
+    for (uint32_t w = 0; w < Wm; w++) ready_[w].store(0);
+    next_.store(0);
+    go_.store(true, std::memory_order_release);
+    std::vector<std::pair<uint32_t, const uint32_t*>> at;
+    for (uint32_t k = 0; k < Wm; k++) at.emplace_back(win_off(pl.d, Wm - 1 - k), nullptr);
+    // outer Horner over the window offsets; the window sums are taken as they become ready (the
+    // caller computes one itself when none is ready yet)
+    Pt acc = pt_identity();
+    bool any = false;
+    for (uint32_t k = 0; k < Wm; k++) {
+      const uint32_t w = Wm - 1 - k;
+      while (!ready_[w].load(std::memory_order_acquire))
+        if (!take_one()) _mm_pause();
+      const Pt& p = sums_[w];
+      const bool ident = fq_is_zero(p.X) && fq_eq(p.Y, p.Z);
+      if (!ident) acc = any ? pt_add(acc, p) : p;
+      any = any || !ident;
+      const uint32_t next = w ? win_off(pl.d, w - 1) : 0u;
+      if (any && win_off(pl.d, w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w) - next));
+    }
+    return acc;
+  }
+
+ private:
+  // One window sum, top window first; false when none is left.
+  bool take_one() {
+    const uint32_t Wm = pl_->d.Wm;
+    const uint32_t k = next_.fetch_add(1);
+    if (k >= Wm) return false;
+    const uint32_t w = Wm - 1 - k;
+    std::vector<std::pair<uint32_t, const uint32_t*>> at;
+    collect_terms(*pl_, terms_, w, w + 1, win_off(pl_->d, w), &at);
+    sums_[w] = horner_run(at, term_at);
+    ready_[w].store(1, std::memory_order_release);
+    return true;
+  }
+  void work() {
+    uint64_t spins = 0;
+    while (!go_.load(std::memory_order_acquire)) {
+      if (quit_.load()) return;
+      if (++spins > 4096) std::this_thread::yield();  // a long device wait: stay cheap
+      else _mm_pause();
+    }
+    while (take_one()) {
+    }
+  }
+  std::vector<std::thread> th_;
+  std::atomic<bool> go_{false}, quit_{false};
+  std::atomic<uint32_t> next_{0};
+  const Plan* pl_ = nullptr;
+  const uint32_t* terms_ = nullptr;
+  std::vector<Pt> sums_;
+  std::unique_ptr<std::atomic<int>[]> ready_;
+};
 
 void pt_to_be_affine(const Pt& p, uint32_t out[16]) {
   uint64_t x[4], y[4];
@@ -917,7 +1013,7 @@ int wait_event(hipStream_t s, hipEvent_t e) {
 // milliseconds, and a blocking wait adds a wake-up latency) and take its window terms.  With
 // `terms` the terms are copied out, so the slot can take its next launch before the host tail
 // runs; otherwise the host tail runs here, on the pinned buffer.
-int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr) {
+int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr, TailCrew* crew = nullptr) {
   Slot& sl = c->slot[si];
   const Plan& pl = sl.pl;
   const auto spin_until = clk::now() + std::chrono::milliseconds(50);
@@ -934,6 +1030,8 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
   auto t0 = clk::now();
   if (terms)
     terms->assign(h, h + outb / 4);
+  else if (crew && crew->active())
+    *result = crew->run(pl, h);
   else
     *result = horner_tail(pl, h);
   auto t1 = clk::now();
@@ -1031,9 +1129,10 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = order_after_user(c, user_stream, 1)) != MSM_OK) return rc;
   c->slot[si].pl = pl;
+  TailCrew crew(tail_helpers());  // started while the device works
   if ((rc = launch_parts(c, pl, splat(d_points), splat(d_scalars), si, PART_ALL, c->slot[si].ws.pts.as<uint32_t>())))
     return rc;
-  return finish_msm(c, si, result);
+  return finish_msm(c, si, result, nullptr, &crew);
 }
 
 // Host -> device copy of one input array on the copy stream, in pieces of `piece` bytes; after
@@ -1110,8 +1209,9 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
   if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
     return fail(rc);
+  TailCrew crew(tail_helpers());
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return fail(rc);
-  return finish_msm(c, si, result);
+  return finish_msm(c, si, result, nullptr, &crew);
 }
 
 // MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
@@ -1943,6 +2043,27 @@ int msm_test_sharded(int mode, const uint32_t* points, const uint32_t* scalars, 
   if (rc != MSM_OK) return rc;
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
+}
+
+// The host tail of a lone MSM of n points (auto plan) on caller-supplied window terms (host
+// Montgomery X|Y|T|Z words, the layout k_bucket_reduce_2 writes): helpers = 0 runs horner_tail,
+// otherwise the TailCrew.  Affine result; *ms = the tail's wall time.
+int msm_test_tail(size_t n, const uint32_t* terms, int helpers, uint32_t out_xy_be[16], double* ms) {
+  Plan pl;
+  if (int rc = make_plan(n, nullptr, 256, &pl)) return rc;
+  TailCrew crew(helpers);
+  const auto t0 = clk::now();
+  const Pt r = helpers ? crew.run(pl, terms) : horner_tail(pl, terms);
+  *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
+// The number of window-term words msm_test_tail reads for n points.
+size_t msm_test_tail_words(size_t n) {
+  Plan pl;
+  if (make_plan(n, nullptr, 256, &pl)) return 0;
+  return (size_t)pl.d.W * pl.nterms * 32;
 }
 
 // Batch field / point ops on the device, canonical LE words.

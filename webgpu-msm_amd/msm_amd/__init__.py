@@ -125,6 +125,8 @@ def load() -> ctypes.CDLL:
         "msm_test_shard_range": ([sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)], ctypes.c_int),
         "msm_test_sharded": ([ctypes.c_int, vp, vp, sz, optp, ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, vp,
                               u32p], ctypes.c_int),
+        "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "msm_test_tail_words": ([sz], sz),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
