@@ -663,8 +663,9 @@ Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
 }
 
 // The tail of a lone MSM (its latency, not a pipeline's throughput, is what counts), spread over
-// helper threads started BEFORE the device finishes (so no thread start-up sits on the critical
-// path; they spin until the terms land).  The helpers compute the window sums
+// helper threads started right after the launch, while the device works (thread start-up before
+// the launch measured +15 us of latency; after it, it overlaps the device; they spin, yielding,
+// until the terms land).  The helpers compute the window sums
 // W_w = sum 2^(pos - off_w) term top window first, while the calling thread runs the outer Horner
 // MSM = sum_w 2^(off_w) W_w, taking each W_w as it becomes ready: ~254 doublings and ~W adds on the
 // critical path instead of ~254 doublings and ~W * nterms adds.  MSM_TAIL_THREADS sets the helper
@@ -1129,9 +1130,9 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = order_after_user(c, user_stream, 1)) != MSM_OK) return rc;
   c->slot[si].pl = pl;
-  TailCrew crew(tail_helpers());  // started while the device works
   if ((rc = launch_parts(c, pl, splat(d_points), splat(d_scalars), si, PART_ALL, c->slot[si].ws.pts.as<uint32_t>())))
     return rc;
+  TailCrew crew(tail_helpers());  // started after the launch: thread start-up overlaps the device
   return finish_msm(c, si, result, nullptr, &crew);
 }
 
@@ -1209,8 +1210,8 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
   if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
     return fail(rc);
-  TailCrew crew(tail_helpers());
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return fail(rc);
+  TailCrew crew(tail_helpers());
   return finish_msm(c, si, result, nullptr, &crew);
 }
 
