@@ -21,6 +21,7 @@
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
 #   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
+#   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
 [ $# -ge 2 ] || { sed -n 2,24p "$0"; exit 2; }
@@ -98,6 +99,13 @@ for step in "$@"; do
           export "$var=$v"
           run "lat_${var}_${v}_$r" 120 python tools/latency_probe.py
           unset "$var"
+        done
+      done ;;
+    latk:*)
+      IFS=: read -r _ ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "latk_${k}_$r" 120 python tools/latency_probe.py --run-length "$k"
         done
       done ;;
     ubench)
