@@ -16,6 +16,7 @@
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
 #   kstats1      the same on one stream (MSM_SLOTS=1), two-MSM 2^20 launches only
+#   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
@@ -73,6 +74,9 @@ for step in "$@"; do
     kstats1)
       MSM_SLOTS=1 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
         -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 20 --warmup 4 --serial-min-s 0 ;;
+    latprof)
+      run latprof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_latprof_d -o run \
+        -- python3 tools/latency_probe.py --runs 12 ;;
     pmc) run pmc 900 bash tools/profile_pmc.sh "$TAG" ;;
     ab:*)
       IFS=: read -r _ libs rounds <<< "$step"
