@@ -3,7 +3,7 @@
 // The reference's host orchestration this replaces:
 //   compute_msm            src/submission/submission.ts:25-157   -> msm_compute / msm_compute_device
 //   getBestWindowSize      submission.ts:18-23                    -> msm_best_window
-//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_lead_scan
+//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_chain_join
 //     (its staging ring, gpu.ts:146-155 / 244-271)                -> upload_points (chunked, overlapped)
 //   split_dynamic          msm-wasm/src/lib.rs:196-202            -> msm_split (host) / k_recode_* (device)
 //   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1/2
@@ -433,7 +433,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(lead_val, nwg * PT_WORDS * 4);
   ENS(lead_open, nwg * 4);
   ENS(cross_key, nwg * 4);
-  ENS(lead_flag, 16);
+  ENS(lead_flag, 16);  // [0] an open lead was seen; [1], [2]: last-workgroup counters (chain join, column scan)
   ENS(skew_list, (nwg + 1) * 4);
   ENS(g_head, pl.runs_max * PT_WORDS * 4);  // touched only by skewed workgroups
   ENS(g_hkey, pl.runs_max * 4);
@@ -535,10 +535,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                          w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
     }
     mark(PH_RECODE);
+    // (its last workgroup also scans the bin totals; lead_flag[2] is its completion counter)
     hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
-                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
-                       d.nbins, w.big_tiles.as<uint32_t>());
+                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
+                       w.big_tiles.as<uint32_t>(), w.lead_flag.as<uint32_t>() + 2);
     mark(PH_SCAN);
     if (d.c <= 16) {
       hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
@@ -570,12 +570,11 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
   if (parts & PART_POST) {
+    // (its last workgroup also chains the leads; lead_flag[1] is its completion counter)
     hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
                        w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
                        w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                       w.lead_flag.as<uint32_t>());
-    hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
-                       w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
+                       w.lead_flag.as<uint32_t>(), w.lead_flag.as<uint32_t>() + 1);
     mark(PH_FIXUP);
     auto red1 = pl.L == 4    ? k_bucket_reduce_1<4>
                 : pl.L == 9  ? k_bucket_reduce_1<9>
@@ -968,14 +967,16 @@ int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Bat
                  int parts, uint32_t* pts) {
   Slot& sl = c->slot[si];
   hipStream_t s = sl.stream;
-  const bool acc = (parts & PART_ACC) != 0;
+  // k_accumulate's bracketing events only when profiling mode 2 reads them: each event-record
+  // node adds ~6 us to the launch sequence's critical path (profiles/r3/latency_timeline.txt)
+  const bool acc = (parts & PART_ACC) != 0 && c->profiling == 2;
   sl.acc_timed = acc;
-  if (parts & (PART_PREP | PART_SORT)) HIPCHECK(hipEventRecord(sl.ev_start, s));
+  if (c->profiling && (parts & (PART_PREP | PART_SORT))) HIPCHECK(hipEventRecord(sl.ev_start, s));
   if (c->profiling == 1) {
     sl.acc_timed = false;
     if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts)) return rc;
   } else if (c->graphs_ok && graphs_enabled()) {
-    Segment* sg = c->graph_events_ok ? get_segment(c, pl, d_points, d_scalars, si, parts, pts, acc) : nullptr;
+    Segment* sg = (!acc || c->graph_events_ok) ? get_segment(c, pl, d_points, d_scalars, si, parts, pts, acc) : nullptr;
     if (sg) {
       HIPCHECK(hipGraphLaunch(sg->exec, s));
     } else {
@@ -989,15 +990,15 @@ int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Bat
         return enqueue_msm(c, pl, d_points, d_scalars, si, s, p, pts);
       };
       if (int rc = run(parts & (PART_PREP | PART_SORT))) return rc;
-      if (acc)
-        if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC, pts, true)) return rc;
+      if (parts & PART_ACC)
+        if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC, pts, acc)) return rc;
       if (int rc = run(parts & PART_POST)) return rc;
     }
   } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts, acc)) {
     return rc;
   }
   if (parts & PART_POST) {
-    HIPCHECK(hipEventRecord(sl.ev_end, s));
+    if (c->profiling) HIPCHECK(hipEventRecord(sl.ev_end, s));
     HIPCHECK(hipEventRecord(sl.ev_done, s));
   }
   return MSM_OK;
