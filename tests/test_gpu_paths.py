@@ -5,6 +5,8 @@ Every expected value is the closed form sum s_i (k_i G) = ((sum s_i k_i) mod r) 
 survey pinned to the Aleo-wasm oracle at 2^12..2^20 (tests/golden/msm_vectors.json); comparisons
 are bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -205,8 +207,12 @@ def test_serial_flag_and_profile():
         M.set_profiling(False)
     assert [as_xy(r) for r in out] == exps
     # every launch is timed (k_accumulate between two events)
-    # 2^16: four MSMs per launch, so the five MSMs take two launches (the last one padded)
-    assert prof["profiled"] == 2 and prof["msms_per_launch"] == 4
+    # 2^16: four MSMs per launch by default, so the five MSMs take two launches (the last one
+    # padded); an MSM_BATCH override (the alternative-configuration reruns) changes the count
+    per = prof["msms_per_launch"]
+    assert prof["profiled"] == -(-5 // per)
+    if "MSM_BATCH" not in os.environ:
+        assert per == 4
     assert 0 < prof["accumulate_sum"] / prof["profiled"] < 50.0
 
 
@@ -224,7 +230,8 @@ def test_eight_msms_per_launch_small_sizes():
     finally:
         M.set_profiling(False)
     assert [as_xy(r) for r in out] == exps
-    assert prof["msms_per_launch"] == 8 and prof["profiled"] == 2
+    if "MSM_BATCH" not in os.environ:  # (an MSM_BATCH override sets the launch size itself)
+        assert prof["msms_per_launch"] == 8 and prof["profiled"] == 2
     out = M.compute_msm_many([M.gen_points(n, k0=3, step=2)] * 13, scs[:13], n)  # 13 % 8 > 4: eight
     assert [as_xy(r) for r in out] == exps[:13]
 
