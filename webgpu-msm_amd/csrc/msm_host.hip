@@ -433,7 +433,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(lead_val, nwg * PT_WORDS * 4);
   ENS(lead_open, nwg * 4);
   ENS(cross_key, nwg * 4);
-  ENS(lead_flag, 16);  // [0] an open lead was seen; [1], [2]: last-workgroup counters (chain join, column scan)
+  ENS(lead_flag, 16);  // [0] an open lead was seen; [1]: k_chain_join's last-workgroup counter
   ENS(skew_list, (nwg + 1) * 4);
   ENS(g_head, pl.runs_max * PT_WORDS * 4);  // touched only by skewed workgroups
   ENS(g_hkey, pl.runs_max * 4);
@@ -535,10 +535,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                          w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
     }
     mark(PH_RECODE);
-    // (its last workgroup also scans the bin totals; lead_flag[2] is its completion counter)
     hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
-                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
-                       w.big_tiles.as<uint32_t>(), w.lead_flag.as<uint32_t>() + 2);
+                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
+                       d.nbins, w.big_tiles.as<uint32_t>());
     mark(PH_SCAN);
     if (d.c <= 16) {
       hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,

@@ -8,8 +8,8 @@
 //   k_recode_digits    signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
 //                      written window-major (= first sort level: one contiguous array per window)
 //   k_part_hist        per (window, chunk) LDS histogram over the window's coarse bucket ranges
-//   k_part_colscan     column prefix sums of the histogram rows -> each chunk's slice of every bin;
-//                      its last workgroup scans the bin totals (bin_scan)
+//   k_part_colscan     column prefix sums of the histogram rows -> each chunk's slice of every bin
+//   k_bin_scan         exclusive scan of the bin totals (one workgroup)
 //   k_part_scatter     digits -> coarse bins (each chunk writes its own contiguous slice per bin)
 //   k_fine_sort        per coarse bin: LDS counting sort by bucket -> (entry, bucket key) lists
 //   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
@@ -341,9 +341,11 @@ constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel 
 // Exclusive scan of colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] = total entries).
 // Also lists the tiles (FS_CAP entries) of bins too big for k_fine_sort's LDS staging:
 // big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
-// (The body of the last k_part_colscan workgroup: 1024 threads.)
-__device__ __forceinline__ void bin_scan(const uint32_t* __restrict__ colsum, uint32_t* __restrict__ bin_base,
-                                         uint32_t nbins, uint32_t* __restrict__ big_tiles) {
+// (A kernel of its own: folding it into k_part_colscan's last workgroup, behind a device-scope
+// fence in every workgroup, measured 6 -> 40-70 us -- each fence writes back the XCD's L2.)
+extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ colsum,
+                                                              uint32_t* __restrict__ bin_base, uint32_t nbins,
+                                                              uint32_t* __restrict__ big_tiles) {
   __shared__ uint32_t part[1024];
   __shared__ uint32_t ntile;
   if (threadIdx.x == 0) ntile = 0;
@@ -383,14 +385,9 @@ __device__ __forceinline__ void bin_scan(const uint32_t* __restrict__ colsum, ui
 
 // Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
 // colsum[w * nbc + bin] = column total.  One workgroup per (64 bins, window); 16 waves split chunks.
-// The last workgroup to finish (a device counter, reset by that workgroup) then runs bin_scan over
-// every column total: one launch, not two, on the sort's dependency chain.
 extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t* __restrict__ hist_rows, MsmDims d,
                                                                   uint32_t* __restrict__ rel,
-                                                                  uint32_t* __restrict__ colsum,
-                                                                  uint32_t* __restrict__ bin_base,
-                                                                  uint32_t* __restrict__ big_tiles,
-                                                                  uint32_t* __restrict__ done) {
+                                                                  uint32_t* __restrict__ colsum) {
   __shared__ uint32_t wsum[16][64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t w = blockIdx.y;
@@ -414,15 +411,6 @@ extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t
     }
     if (wave == 15) colsum[w * d.nbc + bin] = run;
   }
-  __shared__ bool last;
-  __threadfence();  // this workgroup's column totals are visible before it is counted
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) *done = 0;  // leaves the counter zeroed for the next MSM
-  __threadfence();
-  bin_scan(colsum, bin_base, d.nbins, big_tiles);
 }
 
 // Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
@@ -1008,8 +996,9 @@ __device__ __forceinline__ void lead_scan(uint32_t* __restrict__ lead_val, const
 // whether the chain leaves the workgroup; log2(256) steps of one point add.  Then every tail
 // owner adds the chain that follows it, and lane 0 publishes the workgroup's lead.
 // With no skewed workgroup no lead can be open (only this kernel opens them): every workgroup
-// returns at once.  Otherwise the last workgroup to finish chains the leads (lead_scan above),
-// which used to be a launch of its own.
+// returns at once, before any fence.  Otherwise the last workgroup to finish chains the leads
+// (lead_scan above), which used to be a launch of its own: -5 us of launch on every MSM's
+// critical path, and the device-scope fences (an L2 write-back each) only with skewed scalars.
 constexpr uint32_t CJ_GRID = 256;  // k_chain_join workgroups (they loop over the skewed list)
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uint32_t* __restrict__ skew_list,
                                          const uint32_t* __restrict__ total_ptr,
