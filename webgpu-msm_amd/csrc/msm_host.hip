@@ -3,7 +3,7 @@
 // The reference's host orchestration this replaces:
 //   compute_msm            src/submission/submission.ts:25-157   -> msm_compute / msm_compute_device
 //   getBestWindowSize      submission.ts:18-23                    -> msm_best_window
-//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_chain_join
+//   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_lead_scan
 //     (its staging ring, gpu.ts:146-155 / 244-271)                -> upload_points (chunked, overlapped)
 //   split_dynamic          msm-wasm/src/lib.rs:196-202            -> msm_split (host) / k_recode_* (device)
 //   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1/2
@@ -433,7 +433,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(lead_val, nwg * PT_WORDS * 4);
   ENS(lead_open, nwg * 4);
   ENS(cross_key, nwg * 4);
-  ENS(lead_flag, 16);  // [0] an open lead was seen; [1]: k_chain_join's last-workgroup counter
+  ENS(lead_flag, 16);
   ENS(skew_list, (nwg + 1) * 4);
   ENS(g_head, pl.runs_max * PT_WORDS * 4);  // touched only by skewed workgroups
   ENS(g_hkey, pl.runs_max * 4);
@@ -570,11 +570,12 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
   if (parts & PART_POST) {
-    // (its last workgroup also chains the leads; lead_flag[1] is its completion counter)
     hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
                        w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
                        w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
-                       w.lead_flag.as<uint32_t>(), w.lead_flag.as<uint32_t>() + 1);
+                       w.lead_flag.as<uint32_t>());
+    hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
+                       w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
     mark(PH_FIXUP);
     auto red1 = pl.L == 4    ? k_bucket_reduce_1<4>
                 : pl.L == 9  ? k_bucket_reduce_1<9>

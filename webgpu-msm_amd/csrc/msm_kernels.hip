@@ -15,8 +15,7 @@
 //   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
 //                      written directly, buckets cut by run boundaries joined through LDS
 //                      (segmented scan for long chains)
-//   k_chain_join       joins the chains of skewed workgroups; its last workgroup chains bucket
-//                      continuations that run through whole workgroups (lead_scan; skew only)
+//   k_lead_scan        chains bucket continuations that run through whole workgroups (skew only)
 //   k_bucket_reduce_1  per (window, chunk of L buckets): running sums -> U_c = sum (i+1) B, T_c = sum B
 //   k_bucket_reduce_2  per (window, term): plain sums R_{w,V} = sum_c U_c, R_{w,k} = sum_{c: bit k} T_c,
 //                      converted to canonical standard form for the host Horner
@@ -328,6 +327,36 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
   }
 }
 
+// Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
+// colsum[w * nbc + bin] = column total.  One workgroup per (64 bins, window); 16 waves split chunks.
+extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t* __restrict__ hist_rows, MsmDims d,
+                                                                  uint32_t* __restrict__ rel,
+                                                                  uint32_t* __restrict__ colsum) {
+  __shared__ uint32_t wsum[16][64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.y;
+  const uint32_t bin = blockIdx.x * 64 + lane;
+  const uint32_t rows = (d.nch + 15) / 16;
+  const uint32_t r0 = wave * rows, r1 = min(d.nch, r0 + rows);
+  const size_t base = (size_t)w * d.nch * d.nbc;
+  uint32_t sum = 0;
+  if (bin < d.nbc)
+    for (uint32_t r = r0; r < r1; r++) sum += hist_rows[base + (size_t)r * d.nbc + bin];
+  wsum[wave][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t v = 0; v < wave; v++) run += wsum[v][lane];
+  if (bin < d.nbc) {
+    for (uint32_t r = r0; r < r1; r++) {
+      const size_t at = base + (size_t)r * d.nbc + bin;
+      const uint32_t h = hist_rows[at];
+      rel[at] = run;
+      run += h;
+    }
+    if (wave == 15) colsum[w * d.nbc + bin] = run;
+  }
+}
+
 // k_fine_sort geometry (also decides which bins k_bin_scan lists for k_big_place)
 #ifndef MSM_FS_THREADS
 #define MSM_FS_THREADS 512
@@ -341,8 +370,6 @@ constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel 
 // Exclusive scan of colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] = total entries).
 // Also lists the tiles (FS_CAP entries) of bins too big for k_fine_sort's LDS staging:
 // big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
-// (A kernel of its own: folding it into k_part_colscan's last workgroup, behind a device-scope
-// fence in every workgroup, measured 6 -> 40-70 us -- each fence writes back the XCD's L2.)
 extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ colsum,
                                                               uint32_t* __restrict__ bin_base, uint32_t nbins,
                                                               uint32_t* __restrict__ big_tiles) {
@@ -381,36 +408,6 @@ extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __
   if (threadIdx.x == 1023) bin_base[nbins] = part[1023];
   __syncthreads();
   if (threadIdx.x == 0) big_tiles[0] = ntile;
-}
-
-// Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
-// colsum[w * nbc + bin] = column total.  One workgroup per (64 bins, window); 16 waves split chunks.
-extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t* __restrict__ hist_rows, MsmDims d,
-                                                                  uint32_t* __restrict__ rel,
-                                                                  uint32_t* __restrict__ colsum) {
-  __shared__ uint32_t wsum[16][64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t w = blockIdx.y;
-  const uint32_t bin = blockIdx.x * 64 + lane;
-  const uint32_t rows = (d.nch + 15) / 16;
-  const uint32_t r0 = wave * rows, r1 = min(d.nch, r0 + rows);
-  const size_t base = (size_t)w * d.nch * d.nbc;
-  uint32_t sum = 0;
-  if (bin < d.nbc)
-    for (uint32_t r = r0; r < r1; r++) sum += hist_rows[base + (size_t)r * d.nbc + bin];
-  wsum[wave][lane] = sum;
-  __syncthreads();
-  uint32_t run = 0;
-  for (uint32_t v = 0; v < wave; v++) run += wsum[v][lane];
-  if (bin < d.nbc) {
-    for (uint32_t r = r0; r < r1; r++) {
-      const size_t at = base + (size_t)r * d.nbc + bin;
-      const uint32_t h = hist_rows[at];
-      rel[at] = run;
-      run += h;
-    }
-    if (wave == 15) colsum[w * d.nbc + bin] = run;
-  }
 }
 
 // Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
@@ -946,59 +943,11 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
            lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
 }
 
-// Chains leads that run through whole workgroups (a bucket spanning three or more workgroups):
-// segmented suffix scan lead_val[g] <- lead_val[g] + lead_val[g+1] + ... while lead_open.  Run by
-// the last k_chain_join workgroup to finish (its 256 threads walk the leads from the end in tiles,
-// through that workgroup's LDS); a no-op unless an open lead was seen.
-__device__ __forceinline__ void lead_scan(uint32_t* __restrict__ lead_val, const uint32_t* __restrict__ lead_open,
-                                          uint32_t nwg, uint32_t (*sv)[PT_WORDS], uint32_t* so) {
-  constexpr uint32_t LS = ACC_THREADS;
-  const uint32_t i = threadIdx.x;
-  const uint32_t ntiles = (nwg + LS - 1) / LS;
-  for (int tile = (int)ntiles - 1; tile >= 0; tile--) {
-    const uint32_t g = (uint32_t)tile * LS + i;
-    // every lead an open lead can reach is valid (an open chain enters the next workgroup's
-    // lane 0); other slots may hold stale data and are never absorbed
-    bool open = g < nwg && lead_open[g] != 0;
-    xyzt v = g < nwg ? load_pt(lead_val + (size_t)g * PT_WORDS) : pt_identity();
-    store_pt_lds(sv[i], v);
-    so[i] = open ? 1u : 0u;
-    __syncthreads();
-    for (uint32_t d = 1; d < LS; d <<= 1) {
-      const bool take = open && i + d < LS && g + d < nwg;
-      xyzt nv;
-      bool nopen = false;
-      if (take) {
-        nv = load_pt_lds(sv[i + d]);
-        nopen = so[i + d] != 0;
-      }
-      __syncthreads();
-      if (take) {
-        v = pt_add(v, nv);
-        open = nopen;
-        store_pt_lds(sv[i], v);
-        so[i] = open ? 1u : 0u;
-      }
-      __syncthreads();
-    }
-    // still open at the tile's end: absorb the (final) value of the next tile's first lead
-    const uint32_t gn = (uint32_t)(tile + 1) * LS;
-    if (open && gn < nwg) v = pt_add(v, load_pt(lead_val + (size_t)gn * PT_WORDS));
-    __syncthreads();
-    if (g < nwg && lead_open[g] != 0) store_pt(lead_val + (size_t)g * PT_WORDS, v);
-    __syncthreads();
-  }
-}
-
 // Joins for workgroups that k_accumulate found to hold a pass-through run (skewed scalars).
 // Segmented suffix scan over the workgroup's heads by pointer jumping: after it, head r holds
 // h_r + h_{r+1} + ... to the end of r's chain (or the workgroup's end), and its pass bit says
 // whether the chain leaves the workgroup; log2(256) steps of one point add.  Then every tail
 // owner adds the chain that follows it, and lane 0 publishes the workgroup's lead.
-// With no skewed workgroup no lead can be open (only this kernel opens them): every workgroup
-// returns at once, before any fence.  Otherwise the last workgroup to finish chains the leads
-// (lead_scan above), which used to be a launch of its own: -5 us of launch on every MSM's
-// critical path, and the device-scope fences (an L2 write-back each) only with skewed scalars.
 constexpr uint32_t CJ_GRID = 256;  // k_chain_join workgroups (they loop over the skewed list)
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uint32_t* __restrict__ skew_list,
                                          const uint32_t* __restrict__ total_ptr,
@@ -1009,10 +958,9 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uin
                                          uint32_t* __restrict__ buckets,
                                          uint32_t* __restrict__ lead_val,
                                          uint32_t* __restrict__ lead_open,
-                                         uint32_t* __restrict__ lead_flag,
-                                         uint32_t* __restrict__ done) {
+                                         uint32_t* __restrict__ lead_flag) {
   const uint32_t nskew = skew_list[0];
-  if (nskew == 0) return;
+  if (blockIdx.x >= nskew) return;
   const uint32_t M = *total_ptr;
   const uint32_t nruns = (M + K - 1) / K;
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
@@ -1064,16 +1012,59 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_chain_join(const uin
   }
   __syncthreads();  // LDS reused by the next listed workgroup
   }
-  __shared__ bool last;
-  __threadfence();  // this workgroup's leads and lead_flag are visible before it is counted
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) *done = 0;  // leaves the counter zeroed for the next MSM
-  __threadfence();
-  if (*(volatile uint32_t*)lead_flag == 0) return;
-  lead_scan(lead_val, lead_open, (nruns + ACC_THREADS - 1) / ACC_THREADS, sh_head, sh_hkey);
+}
+
+// Chains leads that run through whole workgroups (a bucket spanning three or more workgroups):
+// segmented suffix scan lead_val[g] <- lead_val[g] + lead_val[g+1] + ... while lead_open.  One
+// workgroup walks the leads from the end in tiles of LS_THREADS; a no-op unless k_accumulate saw
+// an open lead.
+constexpr uint32_t LS_THREADS = 512;
+extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* __restrict__ lead_val,
+                                                                     const uint32_t* __restrict__ lead_open,
+                                                                     const uint32_t* __restrict__ lead_flag,
+                                                                     const uint32_t* __restrict__ total_ptr,
+                                                                     uint32_t K) {
+  if (*lead_flag == 0) return;
+  __shared__ uint32_t sv[LS_THREADS][PT_WORDS];
+  __shared__ uint32_t so[LS_THREADS];
+  const uint32_t M = *total_ptr;
+  const uint32_t nruns = (M + K - 1) / K;
+  const uint32_t nwg = (nruns + ACC_THREADS - 1) / ACC_THREADS;
+  const uint32_t i = threadIdx.x;
+  const uint32_t ntiles = (nwg + LS_THREADS - 1) / LS_THREADS;
+  for (int tile = (int)ntiles - 1; tile >= 0; tile--) {
+    const uint32_t g = (uint32_t)tile * LS_THREADS + i;
+    // every lead an open lead can reach is valid (an open chain enters the next workgroup's
+    // lane 0); other slots may hold stale data and are never absorbed
+    bool open = g < nwg && lead_open[g] != 0;
+    xyzt v = g < nwg ? load_pt(lead_val + (size_t)g * PT_WORDS) : pt_identity();
+    store_pt_lds(sv[i], v);
+    so[i] = open ? 1u : 0u;
+    __syncthreads();
+    for (uint32_t d = 1; d < LS_THREADS; d <<= 1) {
+      const bool take = open && i + d < LS_THREADS && g + d < nwg;
+      xyzt nv;
+      bool nopen = false;
+      if (take) {
+        nv = load_pt_lds(sv[i + d]);
+        nopen = so[i + d] != 0;
+      }
+      __syncthreads();
+      if (take) {
+        v = pt_add(v, nv);
+        open = nopen;
+        store_pt_lds(sv[i], v);
+        so[i] = open ? 1u : 0u;
+      }
+      __syncthreads();
+    }
+    // still open at the tile's end: absorb the (final) value of the next tile's first lead
+    const uint32_t gn = (uint32_t)(tile + 1) * LS_THREADS;
+    if (open && gn < nwg) v = pt_add(v, load_pt(lead_val + (size_t)gn * PT_WORDS));
+    __syncthreads();
+    if (g < nwg && lead_open[g] != 0) store_pt(lead_val + (size_t)g * PT_WORDS, v);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
