@@ -15,17 +15,19 @@
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
-#   kstats1      the same on one stream (MSM_SLOTS=1), two-MSM 2^20 launches only
+#   kstats1      the same on one stream (MSM_SLOTS=1), two-MSM 2^20 launches only (the serial pass
+#                warms the GPU first, so the trace averages the launches kernel_ms measures)
 #   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
 #   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
+#   latlib:LIBS[:R]  single-MSM latency over in-tree library variants
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
-[ $# -ge 2 ] || { sed -n 2,24p "$0"; exit 2; }
+[ $# -ge 2 ] || { sed -n 2,28p "$0"; exit 2; }
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -73,7 +75,7 @@ for step in "$@"; do
         -- python3 bench.py ;;
     kstats1)
       MSM_SLOTS=1 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
-        -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 20 --warmup 4 --serial-min-s 0 ;;
+        -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 40 --warmup 10 ;;
     latprof)
       run latprof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_latprof_d -o run \
         -- python3 tools/latency_probe.py --runs 12 ;;
@@ -103,6 +105,13 @@ for step in "$@"; do
           export "$var=$v"
           run "lat_${var}_${v}_$r" 120 python tools/latency_probe.py
           unset "$var"
+        done
+      done ;;
+    latlib:*)
+      IFS=: read -r _ libs rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-3}"); do
+        for lib in ${libs//,/ }; do
+          MSM_AMD_LIB=$LIBDIR/$lib run "latlib_${lib%.so}_$r" 120 python tools/latency_probe.py
         done
       done ;;
     latk:*)
