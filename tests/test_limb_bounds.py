@@ -20,6 +20,7 @@ MASK = (1 << LB) - 1
 R = 1 << 261
 P29 = [(P >> (LB * i)) & MASK for i in range(NL)]
 K8P29 = [536870920, 610271231, 536871443, 661646591, 939568340, 880373981, 718018184, 1050291364, 9788201]
+K5P29 = [536870917, 851181567, 536871243, 681964575, 654339076, 550233738, 717196821, 991976422, 6117625]
 
 
 class B:
@@ -42,7 +43,7 @@ def value_of(limbs):
     return sum(x << (LB * i) for i, x in enumerate(limbs))
 
 
-WIDE_ALL, WIDE_GH, WIDE_EH = 0xFF, 0xE7, 0xBF  # fp29.cuh: steps with a 32-bit reduction digit
+WIDE_ALL, WIDE_GH, WIDE_EH, WIDE_EF = 0xFF, 0xE7, 0xBF, 0xEF  # fp29.cuh: steps with a 32-bit digit
 
 
 def seed(wide: int, k: int) -> int:
@@ -145,6 +146,14 @@ def fe_sub_u(a: B, b: B) -> B:
     return B([x + k for x, k in zip(a.l, K8P29)], a.v + 8 * P)
 
 
+def fe_sub_v(a: B, b: B) -> B:
+    """a + 5p - b (fp29.cuh fe_sub_v): b must be an fe_mul output (normalised, < 2p)."""
+    for i in range(NL):
+        assert K5P29[i] >= b.l[i], "fe_sub_v: negative limb possible"
+    assert b.v <= 2 * P  # B.v is an exclusive bound
+    return B([x + k for x, k in zip(a.l, K5P29)], a.v + 5 * P)
+
+
 def fe_norm(a: B) -> B:
     return B.normalised(a.v)
 
@@ -155,10 +164,11 @@ def fe_sub(a: B, b: B) -> B:
     return fe_norm(fe_sub_u(a, b))
 
 
-def fe_neg_u(b: B) -> B:  # pre_neg_if's unnormalised 8p - kt
+def fe_neg_v(b: B) -> B:  # pre_neg_if's unnormalised 5p - kt
     for i in range(NL):
-        assert K8P29[i] >= b.l[i]
-    return B(list(K8P29), 8 * P)
+        assert K5P29[i] >= b.l[i]
+    assert b.v <= 2 * P  # B.v is an exclusive bound
+    return B(list(K5P29), 5 * P)
 
 
 # point coordinates are always fe_mul outputs (or the identity's normalised constants)
@@ -167,29 +177,52 @@ ONE29 = 536870474 + (276299775 << 29)  # value of Montgomery one is < p; covered
 
 
 def test_madd_bounds():
-    # pre-point record from k_prepare_points: ymx = fe_sub (normalised), ypx = fe_add_n, kt = fe_mul
+    # halved record from k_prepare_points: ymx = fe_sub (normalised), ypx = fe_add_n, kt = fe_mul
     ymx = fe_sub(N_MUL, N_MUL)
     ypx = fe_norm(fe_add(N_MUL, N_MUL))
     kt = N_MUL
     for neg in (False, True):
         q_ymx, q_ypx = (ypx, ymx) if neg else (ymx, ypx)
-        q_kt = fe_neg_u(kt) if neg else kt
+        q_kt = fe_neg_v(kt) if neg else kt
         p = PT
-        A = fe_mul(fe_sub_u(p["Y"], p["X"]), q_ymx)
+        A = fe_mul(fe_sub_v(p["Y"], p["X"]), q_ymx)
         Bv = fe_mul(fe_add(p["Y"], p["X"]), q_ypx)
         C = fe_mul(p["T"], q_kt)
-        D = fe_add(p["Z"], p["Z"])
-        E = fe_sub_u(Bv, A)
-        F = fe_sub(D, C)
-        G = fe_add(D, C)
+        E = fe_sub_v(Bv, A)
+        F = fe_sub_v(p["Z"], C)
+        G = fe_add(p["Z"], C)
         H = fe_add(Bv, A)
-        fe_mul(E, F)
-        fe_mul(G, H, WIDE_GH)
-        fe_mul(E, H, WIDE_EH)
+        fe_mul(E, F, WIDE_EF)
+        fe_mul(G, H)
+        fe_mul(E, H)
         fe_mul(F, G)
 
 
+def test_halved_record_is_the_same_point():
+    """pt_madd with the halved record ((y-x)/2, (y+x)/2, d t) and D = Z1 returns the textbook
+    add-2008-hwcd-3 sum (2d, D = 2 Z1) scaled by 1/4: the same projective point."""
+    import random
+    rnd = random.Random(3)
+    d = 3021
+    inv2 = pow(2, -1, P)
+    for _ in range(50):
+        X1, Y1, Z1 = (rnd.randrange(1, P) for _ in range(3))
+        T1 = X1 * Y1 * pow(Z1, -1, P) % P
+        x2, y2 = rnd.randrange(1, P), rnd.randrange(1, P)
+        t2 = x2 * y2 % P
+        # textbook
+        A = (Y1 - X1) * (y2 - x2); Bv = (Y1 + X1) * (y2 + x2); C = T1 * 2 * d * t2; D = 2 * Z1
+        E, F, G, H = Bv - A, D - C, D + C, Bv + A
+        ref = [v % P for v in (E * F, G * H, E * H, F * G)]
+        # halved record, D = Z1
+        A = (Y1 - X1) * (y2 - x2) * inv2; Bv = (Y1 + X1) * (y2 + x2) * inv2; C = T1 * d * t2; D = Z1
+        E, F, G, H = Bv - A, D - C, D + C, Bv + A
+        got = [v % P for v in (E * F, G * H, E * H, F * G)]
+        assert all(g * 4 % P == r for g, r in zip(got, ref))
+
+
 def padd_operands():
+    """pt_add_quad's operands (U-form differences, as before pt_add moved to the V form)."""
     p = q = PT
     A = fe_mul(fe_sub_u(p["Y"], p["X"]), fe_sub(q["Y"], q["X"]))
     Bv = fe_mul(fe_add(p["Y"], p["X"]), fe_add(q["Y"], q["X"]))
@@ -204,10 +237,19 @@ def padd_operands():
 
 
 def test_padd_bounds():
-    E, F, G, H = padd_operands()
+    p = q = PT
+    A = fe_mul(fe_sub_v(p["Y"], p["X"]), fe_sub_v(q["Y"], q["X"]), WIDE_EF)
+    Bv = fe_mul(fe_add(p["Y"], p["X"]), fe_add(q["Y"], q["X"]))
+    C = fe_mul_2d(fe_mul(p["T"], q["T"]))
+    D0 = fe_mul(p["Z"], q["Z"])
+    D = fe_add(D0, D0)
+    E = fe_sub_v(Bv, A)
+    F = fe_sub(D, C)
+    G = fe_add(D, C)
+    H = fe_add(Bv, A)
     fe_mul(E, F)
     fe_mul(G, H, WIDE_GH)
-    fe_mul(E, H, WIDE_EH)
+    fe_mul(E, H)
     fe_mul(F, G)
 
 
@@ -241,8 +283,8 @@ def test_quad_add_bounds():
 def test_wide_masks_are_maximal():
     """The masks in fp29.cuh are the widest the column budget allows for their operand forms."""
     N = N_MUL
-    G, H, E = fe_add(fe_add(N, N), N), fe_add(N, N), fe_sub_u(N, N)
-    for (a, b), mask in (((G, H), WIDE_GH), ((E, H), WIDE_EH)):
+    G, H, E, V = fe_add(fe_add(N, N), N), fe_add(N, N), fe_sub_u(N, N), fe_sub_v(N, N)
+    for (a, b), mask in (((G, H), WIDE_GH), ((E, H), WIDE_EH), ((V, V), WIDE_EF)):
         fe_mul(a, b, mask)
         for extra in range(8):
             if not (mask >> extra) & 1:
@@ -266,13 +308,15 @@ def test_fe_mul_exact_model():
     cases = []
     for _ in range(3000):
         cases.append((limbs_of(rnd.randrange(2 * P)), limbs_of(rnd.randrange(2 * P)), rnd.choice(
-            (WIDE_ALL, WIDE_GH, WIDE_EH, WIDE_GH & WIDE_EH, 0))))
+            (WIDE_ALL, WIDE_GH, WIDE_EH, WIDE_EF, WIDE_GH & WIDE_EH, 0))))
     # unnormalised operands at their forms' maxima (value = sum of limbs 2^(29 i), kept < 2^257)
     top = (1 << 257) >> (LB * (NL - 1))
     s_max = [(1 << 30) - 1] * (NL - 1) + [top // 2]
     g_max = [3 * (1 << 29) // 2] * (NL - 1) + [top // 4]
     u_max = [x + k - 1 for x, k in zip([0] * NL, K8P29)]
-    for a, b, w in ((g_max, s_max, WIDE_GH), (u_max, s_max, WIDE_EH), (s_max, s_max, WIDE_ALL)):
+    v_max = [MASK + k for k in K5P29[:NL - 1]] + [((2 * P) >> (LB * (NL - 1))) + K5P29[NL - 1]]
+    for a, b, w in ((g_max, s_max, WIDE_GH), (u_max, s_max, WIDE_EH), (s_max, s_max, WIDE_ALL),
+                    (v_max, v_max, WIDE_EF), (v_max, s_max, WIDE_ALL)):
         cases.append((a, b, w))
     for a, b, w in cases:
         r = fe_mul_exact(a, b, w)
@@ -302,6 +346,8 @@ def test_pdbl_bounds():
 def test_model_matches_header_constants():
     assert value_of(K8P29) == 8 * P
     assert all(k >= MASK for k in K8P29[:8])
+    assert value_of(K5P29) == 5 * P
+    assert all(k >= MASK for k in K5P29[:8]) and K5P29[8] >= (2 * P - 1) >> (LB * 8)
     assert P29 == [1, 277610496, 66, 351141280, 452990362, 110046747, 358187729, 198395284, 1223525]
 
 
@@ -329,10 +375,12 @@ REVIEWED = {
     ("fp29.cuh", "fe_mul_2d"): "b9f5c6afdcbc7ff4",
     ("fp29.cuh", "P29"): "b4babf5a3c9d7331",
     ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
-    ("ec.cuh", "pt_madd"): "105059873268fc45",
-    ("ec.cuh", "pt_add"): "c6352f37d81bec89",
+    ("fp29.cuh", "K5P29"): "f3dc542f8a39d740",
+    ("fp29.cuh", "fe_sub_v"): "b95cf1f871e652b6",
+    ("ec.cuh", "pt_madd"): "9b3453a645881673",
+    ("ec.cuh", "pt_add"): "1449f0a88822c610",
     ("ec.cuh", "pt_dbl"): "784353f9934ef437",
-    ("ec.cuh", "pre_neg_if"): "a318c90204dc7c80",
+    ("ec.cuh", "pre_neg_if"): "aa8719a3c1144d3b",
     ("ec.cuh", "pt_add_quad"): "875eba21c1f11e82",
 }
 
@@ -364,4 +412,4 @@ def test_mirrored_sources_unchanged():
 def test_wide_mask_constants_match_header():
     src = open(os.path.join(_CSRC, "fp29.cuh")).read()
     got = {k: int(v, 16) for k, v in re.findall(r"constexpr uint32_t (WIDE_[A-Z]+) = (0x[0-9A-Fa-f]+)u;", src)}
-    assert got == {"WIDE_ALL": WIDE_ALL, "WIDE_GH": WIDE_GH, "WIDE_EH": WIDE_EH}
+    assert got == {"WIDE_ALL": WIDE_ALL, "WIDE_GH": WIDE_GH, "WIDE_EH": WIDE_EH, "WIDE_EF": WIDE_EF}

@@ -8,6 +8,7 @@
 # times out or fails (no GPU step after a fault).  Steps:
 #   tests        the -m gpu parity suites (libmsm.so)
 #   tests_alt    the same with eager launches, then with one slot and one MSM per launch
+#   testslib:LIBS  the parity suites (random sweep aside) against in-tree library variants
 #   bench        python bench.py (the driver's command)
 #   bench50      50 timed steps, no extras
 #   sizes        pipelined ms per MSM at 2^16..2^19 (20 and 50 steps)
@@ -15,8 +16,10 @@
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
-#   kstats1      the same on one stream (MSM_SLOTS=1), two-MSM 2^20 launches only (the serial pass
-#                warms the GPU first, so the trace averages the launches kernel_ms measures)
+#   kstats1      the same on one stream, kernels in order (MSM_SLOTS=1 MSM_FORK_PREP=0), two-MSM 2^20
+#                launches only (the serial pass warms the GPU first, so the trace averages the
+#                launches kernel_ms measures)
+#   kstats1lib:LIBS  kstats1 for each in-tree library variant
 #   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
@@ -27,7 +30,7 @@
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
-[ $# -ge 2 ] || { sed -n 2,28p "$0"; exit 2; }
+[ $# -ge 2 ] || { sed -n 2,31p "$0"; exit 2; }
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -57,6 +60,11 @@ for step in "$@"; do
     tests_alt)
       MSM_NO_GRAPH=1 run tests_eager 900 "${PYTEST[@]}" -k "not random_sweep"
       MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 "${PYTEST[@]}" -k "not random_sweep" ;;
+    testslib:*)
+      IFS=: read -r _ libs <<< "$step"
+      for lib in ${libs//,/ }; do
+        MSM_AMD_LIB=$LIBDIR/$lib run "tests_${lib%.so}" 900 "${PYTEST[@]}" -k "not random_sweep"
+      done ;;
     bench) run bench 300 python bench.py ;;
     bench50) run bench50 300 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" ;;
     sizes)
@@ -74,8 +82,15 @@ for step in "$@"; do
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;
     kstats1)
-      MSM_SLOTS=1 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
+      MSM_SLOTS=1 MSM_FORK_PREP=0 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
         -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 40 --warmup 10 ;;
+    kstats1lib:*)
+      IFS=: read -r _ libs <<< "$step"
+      for lib in ${libs//,/ }; do
+        MSM_SLOTS=1 MSM_FORK_PREP=0 MSM_AMD_LIB=$LIBDIR/$lib run "kstats1_${lib%.so}" 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "gpurun_out/${TAG}_kstats1_${lib%.so}_d" -o run -- python3 bench.py --no-extras \
+          "${BENCH_Q[@]}" --steps 40 --warmup 10
+      done ;;
     latprof)
       run latprof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_latprof_d -o run \
         -- python3 tools/latency_probe.py --runs 12 ;;

@@ -5,7 +5,8 @@
 // non-square mod p, so the unified add-2008-hwcd-3 formulas below are complete: one branch-free
 // path covers P+Q, P+P and the identity (0:1:0:1).  The reference's add_points
 // (curve.wgsl:36-63) computes the same group law with 9 multiplies; here:
-//   * madd (mixed, Q in precomputed affine form (y-x, y+x, 2d*t), z = 1): 7M — the bucket hot loop;
+//   * madd (mixed, Q in halved precomputed affine form ((y-x)/2, (y+x)/2, d*t), z = 1): 7M — the
+//     bucket hot loop;
 //   * padd (projective + projective): 9M;
 //   * pdbl (dbl-2008-hwcd): 4M + 4S.
 #pragma once
@@ -16,7 +17,8 @@ namespace msm {
 struct xyzt {
   fe X, Y, T, Z;
 };
-// Precomputed affine point: (y - x, y + x, 2d*t).  Negation swaps the first two and negates kt.
+// Precomputed affine point, halved: ((y - x)/2, (y + x)/2, d*t) (pt_madd).  Negation swaps the
+// first two and negates kt.
 struct pre {
   fe ymx, ypx, kt;
 };
@@ -30,39 +32,41 @@ __device__ __forceinline__ xyzt pt_identity() {
   return r;
 }
 
-// acc + q (q affine precomputed).  add-2008-hwcd-3 with Z2 = 1, k = 2d.  All outputs normalised.
+// acc + q (q a halved precomputed affine point, below).  add-2008-hwcd-3 with Z2 = 1, k = 2d.
+// The record holds ((y-x)/2, (y+x)/2, d*t): A, B and C come out halved, so D = 2 Z1 / 2 = Z1 needs
+// no doubling, and (X3:Y3:T3:Z3) is the sum with every coordinate scaled by 1/4 -- the same
+// projective point.  Differences carry 5p (V form) and stay unnormalised.  All outputs normalised.
 __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
-  fe A = fe_mul(fe_sub_u(p.Y, p.X), q.ymx);  // U*N
+  fe A = fe_mul(fe_sub_v(p.Y, p.X), q.ymx);  // V*N
   fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);    // S*N
-  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*U for a negated q, pre_neg_if)
-  fe D = fe_add(p.Z, p.Z);                   // 2N: limbs < 2^30, left unnormalised
-  fe E = fe_sub_u(B, A);                     // U (meets F: N and H: S only)
-  fe F = fe_sub(D, C);                       // N
-  fe G = fe_add(D, C);                       // 2N + N: limbs < 1.5 * 2^30 (meets H: S and F: N only)
+  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*V for a negated q, pre_neg_if)
+  fe E = fe_sub_v(B, A);                     // V
+  fe F = fe_sub_v(p.Z, C);                   // V
+  fe G = fe_add(p.Z, C);                     // S
   fe H = fe_add(B, A);                       // S
   xyzt r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul_w<WIDE_GH>(G, H);  // S x 1.5-form: fewer 32-bit reduction digits (fp29.cuh)
-  r.T = fe_mul_w<WIDE_EH>(E, H);  // U x S
-  r.Z = fe_mul(F, G);
+  r.X = fe_mul_w<WIDE_EF>(E, F);  // V x V: one 29-bit reduction digit more (fp29.cuh)
+  r.Y = fe_mul(G, H);             // S x S
+  r.T = fe_mul(E, H);             // V x S
+  r.Z = fe_mul(F, G);             // V x S
   return r;
 }
 
 // p + q, both extended projective.  add-2008-hwcd-3, k = 2d: 9M (the k multiply is fe_mul_2d).
 __device__ __forceinline__ xyzt pt_add(const xyzt& p, const xyzt& q) {
-  fe A = fe_mul(fe_sub_u(p.Y, p.X), fe_sub(q.Y, q.X));  // U*N
+  fe A = fe_mul_w<WIDE_EF>(fe_sub_v(p.Y, p.X), fe_sub_v(q.Y, q.X));  // V*V
   fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));  // S*S
   fe C = fe_mul_2d(fe_mul(p.T, q.T));  // k = 2d = 6042: scaled, not multiplied (value < 3p)
   fe D = fe_mul(p.Z, q.Z);
-  D = fe_add(D, D);  // 2N, unnormalised (see pt_madd)
-  fe E = fe_sub_u(B, A);
-  fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
+  D = fe_add(D, D);  // 2N, unnormalised
+  fe E = fe_sub_v(B, A);  // V
+  fe F = fe_sub(D, C);    // N
+  fe G = fe_add(D, C);    // 2N + N: limbs < 1.5 * 2^30 (meets H: S and F: N only)
+  fe H = fe_add(B, A);    // S
   xyzt r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul_w<WIDE_GH>(G, H);
-  r.T = fe_mul_w<WIDE_EH>(E, H);
+  r.X = fe_mul(E, F);             // V x N
+  r.Y = fe_mul_w<WIDE_GH>(G, H);  // 1.5-form x S: fewer 32-bit reduction digits (fp29.cuh)
+  r.T = fe_mul(E, H);             // V x S
   r.Z = fe_mul(F, G);
   return r;
 }
@@ -86,21 +90,14 @@ __device__ __forceinline__ xyzt pt_dbl(const xyzt& p) {
   return r;
 }
 
-__device__ __forceinline__ xyzt pt_neg(const xyzt& p) {
-  xyzt r = p;
-  r.X = fe_neg(p.X);
-  r.T = fe_neg(p.T);
-  return r;
-}
-
-// -q = (-x, y): swap (y - x, y + x) and negate 2dt.  The negated kt = 8p - kt is left
-// unnormalised (U form, limbs < 2^30), legal as pt_madd's C = T * kt operand (N * U).
+// -q = (-x, y): swap (y - x, y + x)/2 and negate d*t.  The negated kt = 5p - kt is left
+// unnormalised (V form), legal as pt_madd's C = T * kt operand (N * V).
 __device__ __forceinline__ pre pre_neg_if(const pre& q, bool neg) {
   pre r;
   r.ymx = fe_sel(neg, q.ymx, q.ypx);
   r.ypx = fe_sel(neg, q.ypx, q.ymx);
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.kt.v[i] = neg ? K8P29[i] - q.kt.v[i] : q.kt.v[i];
+  for (int i = 0; i < NL; i++) r.kt.v[i] = neg ? K5P29[i] - q.kt.v[i] : q.kt.v[i];
   return r;
 }
 

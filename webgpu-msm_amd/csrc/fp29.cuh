@@ -13,7 +13,8 @@
 // needs no final subtraction.  Additions are limb-wise with no carry; subtractions add a
 // redundant multiple of p whose limbs dominate any normalised limb, then renormalise.
 // Limb forms: "N" = normalised (limbs < 2^29), "S" = sum of two N (limbs < 2^30), "U" = an
-// unnormalised difference (limbs < 1.48 * 2^30).  Each 64-bit column holds up to 9 limb products
+// unnormalised difference over 8p (limbs < 1.48 * 2^30), "V" = one over 5p (limbs < 1.43 * 2^30,
+// fe_sub_v).  Each 64-bit column holds up to 9 limb products
 // plus the reduction products (fe_mul_w: up to 2^32 * p_j), so which operand forms may meet is
 // decided per call site by tests/test_limb_bounds.py (every column < 2^64, worst case over the
 // per-limb maxima).  Values entering fe_mul stay < 2^257.
@@ -41,12 +42,20 @@ __device__ constexpr uint32_t R2_29[NL] = {102099907u, 496719628u, 421467643u, 1
 // R mod p = Montgomery form of 1.
 __device__ constexpr uint32_t ONE29[NL] = {536870474u, 276299775u, 536841777u, 282071103u, 232458597u,
                                            117906524u, 416951824u, 75953059u, 966800u};
-// 2d*R mod p: Montgomery form of k = 2d = 6042 (add-2008-hwcd-3's constant).
-__device__ constexpr uint32_t K2D29[NL] = {534219742u, 493355007u, 360522798u, 7852223u, 582682u,
-                                           196969042u, 170238326u, 321828089u, 296340u};
-// 2d*R^2 mod p: fe_mul(t_std, K2D_R2) = Montgomery form of 2d*t straight from standard form.
-__device__ constexpr uint32_t K2D_R2_29[NL] = {22956135u, 32535989u, 128498189u, 216570651u, 307994937u,
-                                               462062068u, 55188476u, 243732681u, 295952u};
+// The point records hold the precomputed affine point halved, ((y-x)/2, (y+x)/2, d*t) (ec.cuh
+// pt_madd), built straight from standard-form coordinates with these:
+// R^2/2 mod p: fe_mul(a_std, R2H_29) = Montgomery form of a/2.
+__device__ constexpr uint32_t R2H_29[NL] = {51049954u, 118729606u, 210733855u, 183658689u, 142015845u,
+                                            186545474u, 213977984u, 423250658u, 1023982u};
+// R/2 mod p: Montgomery form of 1/2.
+__device__ constexpr uint32_t HALF29[NL] = {536870693u, 406585343u, 536856344u, 409471007u, 116229298u,
+                                            58953262u, 476911368u, 37976529u, 483400u};
+// d*R^2 mod p: fe_mul(t_std, KD_R2_29) = Montgomery form of d*t (d = 3021).
+__device__ constexpr uint32_t KD_R2_29[NL] = {279913524u, 423508698u, 332684583u, 15420509u, 112057194u,
+                                              17618952u, 475123559u, 489499438u, 759738u};
+// d*R mod p: Montgomery form of d.
+__device__ constexpr uint32_t KD29[NL] = {535545327u, 246677503u, 448696855u, 3926111u, 291341u,
+                                          98484521u, 353554619u, 160914044u, 148170u};
 // 2^256 mod p (standard form): fe_mul(a_mont, R256_29) = a * 2^256 mod p, i.e. the host's
 // 4x64-bit Montgomery representation (hostfield.h, R = 2^256) of a.
 __device__ constexpr uint32_t R256_29[NL] = {536870899u, 149159935u, 536870047u, 267001567u, 16705317u,
@@ -55,6 +64,11 @@ __device__ constexpr uint32_t R256_29[NL] = {536870899u, 149159935u, 536870047u,
 // for normalised b.
 __device__ constexpr uint32_t K8P29[NL] = {536870920u, 610271231u, 536871443u, 661646591u, 939568340u,
                                            880373981u, 718018184u, 1050291364u, 9788201u};
+// 5p in a redundant form with limbs 0..7 >= 2^29-1 and limb 8 above the top limb of any value
+// < 2p, so (a + K5P - b) never goes negative limb-wise for b an fe_mul output: pt_madd's
+// differences (the "V" form, fe_sub_v), whose small limbs let them meet each other in a multiply.
+__device__ constexpr uint32_t K5P29[NL] = {536870917u, 851181567u, 536871243u, 681964575u, 654339076u,
+                                           550233738u, 717196821u, 991976422u, 6117625u};
 
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * b + c;
@@ -98,15 +112,17 @@ __device__ __forceinline__ fe fe_one() { return fe_const(ONE29); }
 //    the result is sum_k m_k 2^(29k) p / 2^261, so a 32-bit m_8 would add up to 8p, while 32-bit
 //    digits below it add at most 2^-26 p -- the result stays < 2p.
 // A 32-bit digit makes its reduction products 8x larger, so the columns near the middle only fit
-// 64 bits for the narrower operand forms: WIDE_ALL for N/S/U x N operands (and S x S), fewer
-// wide steps for the two products of pt_madd / pt_add with an S operand against a 1.5-form or
-// U one (tests/test_limb_bounds.py proves every call site's columns < 2^64).
+// 64 bits for the narrower operand forms: WIDE_ALL for N/S/U/V x N operands, S x S and V x S,
+// fewer wide steps for the V x V products (pt_madd's E F, pt_add's A) and for the products with
+// an S operand against a 1.5-form or U one (tests/test_limb_bounds.py proves every call site's
+// columns < 2^64).
 #ifndef MSM_NARROW_DIGITS  // A/B builds only: -DMSM_NARROW_DIGITS gives every step a 29-bit digit
 constexpr uint32_t WIDE_ALL = 0xFFu;  // steps 0..7 wide
 constexpr uint32_t WIDE_GH = 0xE7u;   // steps 0, 1, 2, 5, 6, 7: G (< 1.5 * 2^30 limbs) x H (S)
-constexpr uint32_t WIDE_EH = 0xBFu;   // steps 0..5, 7:          E (U) x H (S)
+constexpr uint32_t WIDE_EH = 0xBFu;   // steps 0..5, 7:          E (U) x H (S) (pt_add_quad)
+constexpr uint32_t WIDE_EF = 0xEFu;   // steps 0..3, 5..7:       pt_madd's E (V) x F (V)
 #else
-constexpr uint32_t WIDE_ALL = 0u, WIDE_GH = 0u, WIDE_EH = 0u;
+constexpr uint32_t WIDE_ALL = 0u, WIDE_GH = 0u, WIDE_EH = 0u, WIDE_EF = 0u;
 #endif
 
 __host__ __device__ constexpr uint64_t fe_mul_seed(uint32_t wide, int k) {
@@ -244,6 +260,14 @@ __device__ __forceinline__ fe fe_sub_u(const fe& a, const fe& b) {
   fe r;
 #pragma unroll
   for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + K8P29[i] - b.v[i];
+  return r;
+}
+// a - b + 5p without renormalisation ("V": limbs < 2^29 + K5P's).  Requires b an fe_mul output
+// (normalised, value < 2p) and a normalised.
+__device__ __forceinline__ fe fe_sub_v(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + K5P29[i] - b.v[i];
   return r;
 }
 // -b (= 8p - b), normalised.

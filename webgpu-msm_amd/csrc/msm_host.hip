@@ -141,12 +141,12 @@ bool plan_eq(const Plan& a, const Plan& b) {
 
 // Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
 struct Workspace {
-  Buf pts, err, digits, hist_rows, rel, colsum, bin_base;
+  Buf pts, err, digits, colsum, bin_base, bin_cur;
   Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets, big_tiles, cursor;
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
   Buf wire_pts, wire_sc;  // device copies of host-resident inputs (msm_compute*, host entries)
   void release() {
-    Buf* bufs[] = {&pts, &err, &digits, &hist_rows, &rel, &colsum, &bin_base, &part_entry, &part_fine,
+    Buf* bufs[] = {&pts, &err, &digits, &colsum, &bin_base, &bin_cur, &part_entry, &part_fine,
                    &sorted_entry, &bucket_start, &run_key, &buckets, &big_tiles, &cursor, &lead_val, &lead_open, &cross_key,
                    &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T, &wire_pts, &wire_sc};
     for (Buf* b : bufs) b->release();
@@ -417,10 +417,9 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(pts, (size_t)(d.shared ? 1 : d.nm) * d.n * PRE_WORDS * 4);
   ENS(err, 16);
   ENS(digits, (size_t)d.W * d.n * 4);
-  ENS(hist_rows, (size_t)d.nch * d.nbins * 4);
-  ENS(rel, (size_t)d.nch * d.nbins * 4);
   ENS(colsum, (size_t)d.nbins * 4);
   ENS(bin_base, ((size_t)d.nbins + 1) * 4);
+  ENS(bin_cur, (size_t)d.nbins * 4);
   ENS(part_entry, pl.Mmax * 4);
   ENS(part_fine, pl.Mmax * 2);
   ENS(sorted_entry, pl.Mmax * 4 + 16);  // + a 16-B tail for k_accumulate's vector entry loads
@@ -442,14 +441,14 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
 #undef ENS
   if (g_alloc_gen.load() != gen0) {
-    // err, lead_flag and hist_rows are kept all-zero between MSMs by the kernels themselves
-    // (k_bucket_reduce_2 clears the flags, k_part_scatter the histogram rows it consumed), so a
+    // err, lead_flag and colsum are kept all-zero between MSMs by the kernels themselves
+    // (k_bucket_reduce_2 clears the flags, k_bin_scan the bin totals it consumed), so a
     // replayed graph needs no memset nodes; fresh allocations start that invariant here.
     hipStream_t st = sl0.stream;
     if (hipMemsetAsync(w.err.p, 0, w.err.cap, st) != hipSuccess ||
         hipMemsetAsync(w.lead_flag.p, 0, w.lead_flag.cap, st) != hipSuccess ||
         hipMemsetAsync(w.skew_list.p, 0, 4, st) != hipSuccess ||
-        hipMemsetAsync(w.hist_rows.p, 0, w.hist_rows.cap, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        hipMemsetAsync(w.colsum.p, 0, w.colsum.cap, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
       return MSM_ERR_HIP;
   }
   const size_t hbytes = (size_t)d.W * pl.nterms * 32 * 4 + 64;
@@ -529,25 +528,23 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     const unsigned rc_grid = grid_for(d.n, RC_SPAN);
     if (d.c <= 16) {
       hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                         w.digits.as<uint16_t>(), w.hist_rows.as<uint32_t>());
+                         w.digits.as<uint16_t>(), w.colsum.as<uint32_t>());
     } else {
       hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                         w.digits.as<uint32_t>(), w.hist_rows.as<uint32_t>());
+                         w.digits.as<uint32_t>(), w.colsum.as<uint32_t>());
     }
     mark(PH_RECODE);
-    hipLaunchKernelGGL(k_part_colscan, dim3(grid_for(d.nbc, 64), d.W), dim3(1024), 0, s, w.hist_rows.as<uint32_t>(), d,
-                       w.rel.as<uint32_t>(), w.colsum.as<uint32_t>());
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, w.colsum.as<uint32_t>(), w.bin_base.as<uint32_t>(),
-                       d.nbins, w.big_tiles.as<uint32_t>());
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(BS_THREADS), 0, s, w.colsum.as<uint32_t>(),
+                       w.bin_base.as<uint32_t>(), w.bin_cur.as<uint32_t>(), d.nbins, w.big_tiles.as<uint32_t>());
     mark(PH_SCAN);
     if (d.c <= 16) {
-      hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                         w.digits.as<uint16_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
-                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
+      hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 8, s,
+                         w.digits.as<uint16_t>(), d, w.bin_cur.as<uint32_t>(), w.part_entry.as<uint32_t>(),
+                         w.part_fine.as<uint16_t>());
     } else {
-      hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
-                         w.digits.as<uint32_t>(), d, w.hist_rows.as<uint32_t>(), w.rel.as<uint32_t>(),
-                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(), w.part_fine.as<uint16_t>());
+      hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 8, s,
+                         w.digits.as<uint32_t>(), d, w.bin_cur.as<uint32_t>(), w.part_entry.as<uint32_t>(),
+                         w.part_fine.as<uint16_t>());
     }
     mark(PH_SCATTER);
     hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
@@ -896,7 +893,7 @@ int repoint_inputs(const Plan& pl, Slot& sl, Segment& sg, const BatchPtrs& d_poi
     BatchPtrs scal = d_scalars;
     MsmDims dd = d;
     void* digits = w.digits.p;
-    uint32_t* hist = w.hist_rows.as<uint32_t>();
+    uint32_t* hist = w.colsum.as<uint32_t>();
     void* a_rc[] = {&scal, &dd, &digits, &hist};
     hipKernelNodeParams kr = sg.p_recode;
     kr.kernelParams = a_rc;

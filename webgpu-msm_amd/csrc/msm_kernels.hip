@@ -3,15 +3,16 @@
 // split / inter-bucket reduce (src/submission/msm-wasm/src/lib.rs:46-133) with one on-device
 // pipeline:
 //
-//   k_prepare_points   wire points (BE x|y|t|z, 128 B) -> precomputed affine (y-x, y+x, 2dt) in
-//                      29-bit Montgomery limbs, 128 B records (one cache line each)
-//   k_recode_digits    signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
-//                      written window-major (= first sort level: one contiguous array per window)
-//   k_part_hist        per (window, chunk) LDS histogram over the window's coarse bucket ranges
-//   k_part_colscan     column prefix sums of the histogram rows -> each chunk's slice of every bin
+//   k_prepare_points   wire points (BE x|y|t|z, 128 B) -> halved precomputed affine records
+//                      ((y-x)/2, (y+x)/2, d t) in 29-bit Montgomery limbs, 128 B (one cache line)
+//   k_recode_hist      signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
+//                      written window-major (= first sort level: one contiguous array per window),
+//                      with the coarse-bin totals (LDS histogram, flushed with global atomics)
 //   k_bin_scan         exclusive scan of the bin totals (one workgroup)
-//   k_part_scatter     digits -> coarse bins (each chunk writes its own contiguous slice per bin)
+//   k_part_scatter     digits -> coarse bins (each chunk reserves and writes one contiguous slice
+//                      per bin)
 //   k_fine_sort        per coarse bin: LDS counting sort by bucket -> (entry, bucket key) lists
+//   k_big_place        tile-parallel placement of bins too big for k_fine_sort (skew only)
 //   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
 //                      written directly, buckets cut by run boundaries joined through LDS
 //                      (segmented scan for long chains)
@@ -114,18 +115,20 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
     z_zero = z_zero && zw[k] == 0u;
   }
   if (live && z_zero) atomicOr(err, MSM_DEV_ERR_BAD_POINT);
-  fe x = fe_to_mont(fe_from_words_le(xw));
-  fe y = fe_to_mont(fe_from_words_le(yw));
-  fe kt;
+  // the halved record (ec.cuh pt_madd): x/2, y/2 and d*t in Montgomery form
+  fe x, y, kt;
   if (z_one) {
-    kt = fe_mul(fe_from_words_le(tw), fe_const(K2D_R2_29));
+    x = fe_mul(fe_from_words_le(xw), fe_const(R2H_29));
+    y = fe_mul(fe_from_words_le(yw), fe_const(R2H_29));
+    kt = fe_mul(fe_from_words_le(tw), fe_const(KD_R2_29));
   } else {
     // Projective input (z != 1, README.md:92 allows it): normalise to affine with one inversion.
     fe zi = fe_inv(fe_to_mont(fe_from_words_le(zw)));
+    fe zh = fe_mul(zi, fe_const(HALF29));
     fe t = fe_mul(fe_to_mont(fe_from_words_le(tw)), zi);
-    x = fe_mul(x, zi);
-    y = fe_mul(y, zi);
-    kt = fe_mul(t, fe_const(K2D29));
+    x = fe_mul(fe_to_mont(fe_from_words_le(xw)), zh);
+    y = fe_mul(fe_to_mont(fe_from_words_le(yw)), zh);
+    kt = fe_mul(t, fe_const(KD29));
   }
   fe ymx = fe_sub(y, x);
   fe ypx = fe_add_n(y, x);
@@ -273,11 +276,11 @@ struct DigitCode<uint32_t> {
   static constexpr uint32_t ZERO = 0xffffffffu, SIGN = 0x80000000u, MAG = 0x7fffffffu, SHIFT = 31;
 };
 
-// Pass 0+1 (fused): each workgroup recodes RC_SPAN scalars (a quarter of one partition chunk of
-// `ch`) into window-major digit codes (the window-major layout is the first sort level for free:
-// each window is one contiguous array) and builds, in LDS, their histogram over every window's
-// nbc coarse bins, flushed with global atomics into hist_rows[w][chunk][bin] (zeroed first).
-// Digits are read back only once, by k_part_scatter.
+// Pass 0+1 (fused): each workgroup recodes RC_SPAN scalars into window-major digit codes (the
+// window-major layout is the first sort level for free: each window is one contiguous array) and
+// builds, in LDS, their histogram over every window's nbc coarse bins, flushed with global
+// atomics into the bin totals colsum[w][bin] (kept zeroed between MSMs by k_bin_scan).  Digits
+// are read back only once, by k_part_scatter.
 #ifndef MSM_PT_THREADS
 #define MSM_PT_THREADS 1024
 #endif
@@ -290,24 +293,25 @@ constexpr uint32_t PS_R = MSM_PS_R;  // digits per lane (ch = PT_THREADS * PS_R)
 #define MSM_RC_THREADS 1024
 #endif
 constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
-constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup (4 per lane)
+constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup
 template <typename T>
 // blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its windows
 // [y Wm, (y+1) Wm).
 __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_sets, MsmDims d,
-                                                            T* __restrict__ digits, uint32_t* __restrict__ hist_rows) {
+                                                            T* __restrict__ digits, uint32_t* __restrict__ colsum) {
   extern __shared__ uint32_t lds_hist[];  // [Wm][nbc]
   const uint32_t* __restrict__ scalars = scalar_sets.p[blockIdx.y];
   const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
-  const uint32_t ck = lo / d.ch;
   const uint32_t w0 = blockIdx.y * d.Wm;
   const uint32_t nh = d.Wm * d.nbc;
   for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) lds_hist[b] = 0;
   __syncthreads();
+  // (loading all of a lane's scalars before recoding any measured slower: 43 vs 37 us per
+  // two-MSM 2^20 launch)
   for (uint32_t i = lo + threadIdx.x; i < hi; i += RC_THREADS) {
-    uint32_t sw[8];
-    load_scalar(scalars, i, sw);
-    recode(sw, d, [&](uint32_t w, int32_t digit) {
+    uint32_t s[8];
+    load_scalar(scalars, i, s);
+    recode(s, d, [&](uint32_t w, int32_t digit) {
       uint32_t code = DigitCode<T>::ZERO;
       if (digit != 0) {
         const uint32_t mag = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
@@ -320,40 +324,7 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) {
     const uint32_t v = lds_hist[b];
-    if (v) {
-      const uint32_t w = b / d.nbc, bin = b - w * d.nbc;
-      atomicAdd(&hist_rows[((size_t)(w0 + w) * d.nch + ck) * d.nbc + bin], v);
-    }
-  }
-}
-
-// Column scan per window: rel[w][chunk][bin] = sum_{chunk' < chunk} hist[w][chunk'][bin],
-// colsum[w * nbc + bin] = column total.  One workgroup per (64 bins, window); 16 waves split chunks.
-extern "C" __global__ void __launch_bounds__(1024) k_part_colscan(const uint32_t* __restrict__ hist_rows, MsmDims d,
-                                                                  uint32_t* __restrict__ rel,
-                                                                  uint32_t* __restrict__ colsum) {
-  __shared__ uint32_t wsum[16][64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t w = blockIdx.y;
-  const uint32_t bin = blockIdx.x * 64 + lane;
-  const uint32_t rows = (d.nch + 15) / 16;
-  const uint32_t r0 = wave * rows, r1 = min(d.nch, r0 + rows);
-  const size_t base = (size_t)w * d.nch * d.nbc;
-  uint32_t sum = 0;
-  if (bin < d.nbc)
-    for (uint32_t r = r0; r < r1; r++) sum += hist_rows[base + (size_t)r * d.nbc + bin];
-  wsum[wave][lane] = sum;
-  __syncthreads();
-  uint32_t run = 0;
-  for (uint32_t v = 0; v < wave; v++) run += wsum[v][lane];
-  if (bin < d.nbc) {
-    for (uint32_t r = r0; r < r1; r++) {
-      const size_t at = base + (size_t)r * d.nbc + bin;
-      const uint32_t h = hist_rows[at];
-      rel[at] = run;
-      run += h;
-    }
-    if (wave == 15) colsum[w * d.nbc + bin] = run;
+    if (v) atomicAdd(&colsum[w0 * d.nbc + b], v);
   }
 }
 
@@ -367,108 +338,149 @@ constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS (5
 constexpr uint32_t FS_MAXF = 2048;
 constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel by k_big_place
 
-// Exclusive scan of colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] = total entries).
-// Also lists the tiles (FS_CAP entries) of bins too big for k_fine_sort's LDS staging:
-// big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
-extern "C" __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ colsum,
-                                                              uint32_t* __restrict__ bin_base, uint32_t nbins,
-                                                              uint32_t* __restrict__ big_tiles) {
-  __shared__ uint32_t part[1024];
-  __shared__ uint32_t ntile;
-  if (threadIdx.x == 0) ntile = 0;
-  const uint32_t per = (nbins + 1023) / 1024;
-  const uint32_t lo = threadIdx.x * per;
-  uint32_t sum = 0;
-  for (uint32_t k = 0; k < per; k++)
-    if (lo + k < nbins) sum += colsum[lo + k];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+// Exclusive scan of the bin totals colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] =
+// total entries), with a copy in bin_cur (k_part_scatter's slice cursors); colsum is left zeroed
+// for the next MSM's atomics.  One workgroup, tiles of BS_TILE bins: a tile is staged in LDS with
+// coalesced loads, each thread scans a contiguous run of it, and the runs' sums are scanned per
+// wave (DPP) and across the 16 waves.  Also lists the tiles (FS_CAP entries) of bins too big for
+// k_fine_sort's LDS staging: big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
+constexpr uint32_t BS_THREADS = 1024;
+constexpr uint32_t BS_TILE = 16384;  // 64 KiB of LDS; a two-MSM 2^20 launch has 8,704 bins
+extern "C" __global__ void __launch_bounds__(BS_THREADS) k_bin_scan(uint32_t* __restrict__ colsum,
+                                                                    uint32_t* __restrict__ bin_base,
+                                                                    uint32_t* __restrict__ bin_cur, uint32_t nbins,
+                                                                    uint32_t* __restrict__ big_tiles) {
+  __shared__ uint32_t sv[BS_TILE];
+  __shared__ uint32_t wtot[BS_THREADS / 64];
+  __shared__ uint32_t ntile, carry;
+  if (threadIdx.x == 0) ntile = carry = 0;
+  const uint32_t wave = threadIdx.x >> 6;
+  for (uint32_t t0 = 0; t0 < nbins; t0 += BS_TILE) {
+    const uint32_t nt = min(BS_TILE, nbins - t0);
+    for (uint32_t b = threadIdx.x; b < nt; b += BS_THREADS) {
+      sv[b] = colsum[t0 + b];
+      colsum[t0 + b] = 0;
+    }
     __syncthreads();
-    part[threadIdx.x] += v;
+    const uint32_t per = (nt + BS_THREADS - 1) / BS_THREADS;
+    const uint32_t lo = min(nt, threadIdx.x * per), hi = min(nt, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; k++) sum += sv[k];
+    uint32_t wsum;
+    const uint32_t wpre = wave_excl_scan(sum, wsum);
+    if ((threadIdx.x & 63) == 0) wtot[wave] = wsum;
     __syncthreads();
-  }
-  uint32_t run = part[threadIdx.x] - sum;
-  for (uint32_t k = 0; k < per; k++) {
-    if (lo + k < nbins) {
-      const uint32_t m = colsum[lo + k];
-      bin_base[lo + k] = run;
+    uint32_t run = carry + wpre;
+    for (uint32_t v = 0; v < wave; v++) run += wtot[v];
+    for (uint32_t k = lo; k < hi; k++) {
+      const uint32_t m = sv[k];
+      sv[k] = run;
       run += m;
       if (m > FS_BIG) {
-        const uint32_t nt = (m + FS_CAP - 1) / FS_CAP;
-        const uint32_t at = atomicAdd(&ntile, nt);
-        for (uint32_t t = 0; t < nt; t++) {
-          big_tiles[1 + 2 * (at + t)] = lo + k;
+        const uint32_t ntl = (m + FS_CAP - 1) / FS_CAP;
+        const uint32_t at = atomicAdd(&ntile, ntl);
+        for (uint32_t t = 0; t < ntl; t++) {
+          big_tiles[1 + 2 * (at + t)] = t0 + k;
           big_tiles[2 + 2 * (at + t)] = t * FS_CAP;
         }
       }
     }
+    __syncthreads();  // every thread has read carry
+    if (threadIdx.x == BS_THREADS - 1) carry = run;
+    for (uint32_t b = threadIdx.x; b < nt; b += BS_THREADS) {
+      const uint32_t v = sv[b];
+      bin_base[t0 + b] = v;
+      bin_cur[t0 + b] = v;
+    }
+    __syncthreads();  // the tile's LDS is reused, carry published
   }
-  if (threadIdx.x == 1023) bin_base[nbins] = part[1023];
-  __syncthreads();
-  if (threadIdx.x == 0) big_tiles[0] = ntile;
+  if (threadIdx.x == 0) {
+    bin_base[nbins] = carry;
+    big_tiles[0] = ntile;
+  }
 }
 
 // Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
-// coarse bin.  The chunk is first counting-sorted by bin inside LDS, then streamed out so that
-// consecutive lanes write consecutive addresses of a slice (>= 64 entries per slice by
-// construction of ch): whole lines, one CU each.
+// coarse bin.  The chunk is counting-sorted by bin inside LDS -- the LDS atomic that counts an
+// entry also returns its rank inside its bin, so every entry is placed without a second atomic
+// -- and each bin's slice is reserved with one global atomic on the bin's cursor (bin_cur, from
+// k_bin_scan; the slices' order inside a bin is immaterial: the bucket sums commute).  The
+// staged chunk is then streamed out so that consecutive lanes write consecutive addresses of a
+// slice (>= 64 entries per slice by construction of ch).  (Writing each entry straight from
+// registers to its slice, with no LDS staging, measured 59 -> 153 us per two-MSM 2^20 launch; the
+// same in k_fine_sort 96 -> 168 us.)
+//
+// Staging keeps 4 B per entry for 16-bit codes: code << 14 | position in the chunk (ch = 2^14),
+// 64 KiB, so two workgroups share a CU; 32-bit codes (c > 16) stage (code, position) pairs.
+template <typename T>
+struct PartStage;
+template <>
+struct PartStage<uint16_t> {
+  using V = uint32_t;
+  static __device__ __forceinline__ V pack(uint32_t code, uint32_t li) { return code << 14 | li; }
+  static __device__ __forceinline__ uint32_t code(V v) { return v >> 14; }
+  static __device__ __forceinline__ uint32_t pos(V v) { return v & 0x3fffu; }
+};
+template <>
+struct PartStage<uint32_t> {
+  using V = uint2;
+  static __device__ __forceinline__ V pack(uint32_t code, uint32_t li) { return make_uint2(code, li); }
+  static __device__ __forceinline__ uint32_t code(V v) { return v.x; }
+  static __device__ __forceinline__ uint32_t pos(V v) { return v.y; }
+};
+static_assert(PT_THREADS * PS_R == (1u << 14), "PartStage<uint16_t> packs a 14-bit chunk position");
+
 template <typename T>
 __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
-                                                                        uint32_t* __restrict__ hist_rows,
-                                                                        const uint32_t* __restrict__ rel,
-                                                                        const uint32_t* __restrict__ bin_base,
-                                                                        uint32_t* __restrict__ part_entry,
-                                                                        uint16_t* __restrict__ part_fine) {
-  // one 8-B slot per staged entry: the output word (low) and fine | bin << 16 (high), so the
-  // scattered LDS write is one ds_write_b64 (three narrow ones measured heavy in bank conflicts)
-  __shared__ uint2 st[PT_THREADS * PS_R];
-  extern __shared__ uint32_t dyn[];  // [nbc] local cursor, [nbc] local start, [nbc] global slice start
-  uint32_t* lcur = dyn;
-  uint32_t* lstart = dyn + d.nbc;
-  uint32_t* gstart = dyn + 2 * d.nbc;
+                                                             uint32_t* __restrict__ bin_cur,
+                                                             uint32_t* __restrict__ part_entry,
+                                                             uint16_t* __restrict__ part_fine) {
+  using S = PartStage<T>;
+  __shared__ typename S::V st[PT_THREADS * PS_R];
+  __shared__ uint32_t m_live;
+  extern __shared__ uint32_t dyn[];  // [nbc] count -> local start, [nbc] global slice start
+  uint32_t* lcnt = dyn;
+  uint32_t* gstart = dyn + d.nbc;
   const uint32_t w = blockIdx.y, ck = blockIdx.x;
   const uint32_t pbase = d.shared ? 0u : (w / d.Wm) * d.n;  // first point record of this window's MSM
-  const size_t row = ((size_t)w * d.nch + ck) * d.nbc;
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
-    lcur[b] = hist_rows[row + b];
-    hist_rows[row + b] = 0;  // consumed: leaves the histogram zeroed for the next MSM's atomics
-    gstart[b] = bin_base[w * d.nbc + b] + rel[row + b];
-  }
-  __syncthreads();
-  lds_excl_scan_wave0(lcur, d.nbc);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lstart[b] = lcur[b];
-  __syncthreads();
-  const uint32_t fmask = (1u << d.fb) - 1u;
   const T* dw = digits + (size_t)w * d.n;
   const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
-  uint32_t code[PS_R];
+  uint32_t code[PS_R], rank[PS_R];
 #pragma unroll
   for (uint32_t r = 0; r < PS_R; r++) {
     const uint32_t i = lo + r * PT_THREADS + threadIdx.x;
     code[r] = i < hi ? (uint32_t)dw[i] : DigitCode<T>::ZERO;
   }
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lcnt[b] = 0;
+  __syncthreads();
 #pragma unroll
-  for (uint32_t r = 0; r < PS_R; r++) {
-    if (code[r] != DigitCode<T>::ZERO) {
-      const uint32_t i = lo + r * PT_THREADS + threadIdx.x;
-      const uint32_t b = code[r] & DigitCode<T>::MAG;
-      const uint32_t bin = b >> d.fb;
-      const uint32_t p = atomicAdd(&lcur[bin], 1u);
-      const uint32_t ent = ((pbase + i) << 1) | (code[r] >> DigitCode<T>::SHIFT), fine = b & fmask;
-      st[p] = make_uint2(d.packed ? (ent << d.fb) | fine : ent, fine | (bin << 16));
-    }
+  for (uint32_t r = 0; r < PS_R; r++)
+    if (code[r] != DigitCode<T>::ZERO) rank[r] = atomicAdd(&lcnt[(code[r] & DigitCode<T>::MAG) >> d.fb], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
+    const uint32_t c = lcnt[b];
+    gstart[b] = c ? atomicAdd(&bin_cur[w * d.nbc + b], c) : 0u;
+    if (b == d.nbc - 1) m_live = c;
   }
   __syncthreads();
-  const uint32_t m = lcur[d.nbc - 1];  // past-the-end of the last bin = live digits of the chunk
+  lds_excl_scan_wave0(lcnt, d.nbc);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < PS_R; r++)
+    if (code[r] != DigitCode<T>::ZERO)
+      st[lcnt[(code[r] & DigitCode<T>::MAG) >> d.fb] + rank[r]] = S::pack(code[r], r * PT_THREADS + threadIdx.x);
+  __syncthreads();
+  const uint32_t m = lcnt[d.nbc - 1] + m_live;  // live digits of the chunk
+  const uint32_t fmask = (1u << d.fb) - 1u;
   for (uint32_t j = threadIdx.x; j < m; j += PT_THREADS) {
-    const uint2 v = st[j];
-    const uint32_t bin = v.y >> 16;
-    const uint32_t dst = gstart[bin] + (j - lstart[bin]);
-    part_entry[dst] = v.x;
-    if (!d.packed) part_fine[dst] = (uint16_t)(v.y & 0xffffu);
+    const typename S::V v = st[j];
+    const uint32_t cd = S::code(v);
+    const uint32_t b = cd & DigitCode<T>::MAG;
+    const uint32_t bin = b >> d.fb, fine = b & fmask;
+    const uint32_t ent = ((pbase + lo + S::pos(v)) << 1) | (cd >> DigitCode<T>::SHIFT);
+    const uint32_t dst = gstart[bin] + (j - lcnt[bin]);
+    part_entry[dst] = d.packed ? (ent << d.fb) | fine : ent;
+    if (!d.packed) part_fine[dst] = (uint16_t)fine;
   }
 }
 
@@ -534,6 +546,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
   }
   __syncthreads();
   const bool staged = m <= FS_CAP;
+  // fk: fine key (< 2^11) of a staged entry, later | its rank in its bucket << 16 (< FS_CAP)
   uint32_t fk[FS_R], en[FS_R];
   if (staged) {
     // every load issued before any is used; the packed/unpacked choice is uniform
@@ -560,7 +573,7 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     }
 #pragma unroll
     for (uint32_t r = 0; r < FS_R; r++)
-      if (fk[r] != 0xffffu) atomicAdd(&cnt[fk[r]], 1u);
+      if (fk[r] != 0xffffu) fk[r] |= atomicAdd(&cnt[fk[r]], 1u) << 16;
   } else {
     // register tiles of FS_R keys per lane (independent loads in flight); runs of equal keys
     // are collapsed before the LDS atomic
@@ -624,12 +637,8 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     return;
   }
 #pragma unroll
-  for (uint32_t r = 0; r < FS_R; r++) {
-    if (fk[r] != 0xffffu) {
-      const uint32_t p = atomicAdd(&cnt[fk[r]], 1u);
-      st_entry[p] = en[r];
-    }
-  }
+  for (uint32_t r = 0; r < FS_R; r++)
+    if (fk[r] != 0xffffu) st_entry[cnt[fk[r] & 0xffffu] + (fk[r] >> 16)] = en[r];
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
 }
@@ -1321,10 +1330,10 @@ __global__ void k_test_point(const uint32_t* __restrict__ p, const uint32_t* __r
   if constexpr (OP == 0) {
     R = pt_add(P, Q);
   } else if constexpr (OP == 1) {
-    pre qq;
-    qq.ymx = fe_sub(Q.Y, Q.X);
-    qq.ypx = fe_add_n(Q.Y, Q.X);
-    qq.kt = fe_mul(Q.T, fe_const(K2D29));
+    pre qq;  // halved, as k_prepare_points writes it
+    qq.ymx = fe_mul(fe_sub(Q.Y, Q.X), fe_const(HALF29));
+    qq.ypx = fe_mul(fe_add_n(Q.Y, Q.X), fe_const(HALF29));
+    qq.kt = fe_mul(Q.T, fe_const(KD29));
     R = pt_madd(P, qq);
   } else {
     R = pt_dbl(P);
