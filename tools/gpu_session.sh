@@ -19,7 +19,7 @@
 #   kstats1      the same on one stream, kernels in order (MSM_SLOTS=1 MSM_FORK_PREP=0), two-MSM 2^20
 #                launches only (the serial pass warms the GPU first, so the trace averages the
 #                launches kernel_ms measures)
-#   kstats1lib:LIBS  kstats1 for each in-tree library variant
+#   kstats1lib:LIBS  kstats1 for each in-tree library variant (names suffixed with $KS if set)
 #   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
@@ -28,9 +28,10 @@
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
 #   latlib:LIBS[:R]  single-MSM latency over in-tree library variants
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
+#   set:VAR=VAL / unset:VAR  environment for the steps that follow (e.g. set:MSM_RED_L=8 kstats1)
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
-[ $# -ge 2 ] || { sed -n 2,31p "$0"; exit 2; }
+[ $# -ge 2 ] || { sed -n 2,32p "$0"; exit 2; }
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -87,8 +88,8 @@ for step in "$@"; do
     kstats1lib:*)
       IFS=: read -r _ libs <<< "$step"
       for lib in ${libs//,/ }; do
-        MSM_SLOTS=1 MSM_FORK_PREP=0 MSM_AMD_LIB=$LIBDIR/$lib run "kstats1_${lib%.so}" 300 rocprofv3 --kernel-trace --stats \
-          --output-format csv -d "gpurun_out/${TAG}_kstats1_${lib%.so}_d" -o run -- python3 bench.py --no-extras \
+        MSM_SLOTS=1 MSM_FORK_PREP=0 MSM_AMD_LIB=$LIBDIR/$lib run "kstats1_${lib%.so}${KS:-}" 300 rocprofv3 --kernel-trace \
+          --stats --output-format csv -d "gpurun_out/${TAG}_kstats1_${lib%.so}${KS:-}_d" -o run -- python3 bench.py --no-extras \
           "${BENCH_Q[@]}" --steps 40 --warmup 10
       done ;;
     latprof)
@@ -136,6 +137,8 @@ for step in "$@"; do
           run "latk_${k}_$r" 120 python tools/latency_probe.py --run-length "$k"
         done
       done ;;
+    set:*) export "${step#set:}" ;;
+    unset:*) unset "${step#unset:}" ;;
     ubench)
       run ubench_fmul 120 tools/ubench/fmul_bench
       run ubench_isa 120 tools/ubench/isa_rates ;;

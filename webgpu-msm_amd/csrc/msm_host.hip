@@ -154,8 +154,13 @@ struct Workspace {
 };
 
 // Launch-sequence parts.  PREP: wire points -> precomputed records; SORT: scalar recoding and the
-// bucket sort; ACC: bucket accumulation; POST: skew joins and the bucket reduction.
-constexpr int PART_PREP = 1, PART_SORT = 2, PART_ACC = 4, PART_POST = 8, PART_ALL = 15;
+// bucket sort; ACC: bucket accumulation; POST: the bucket reduction; JOIN: the joins of skewed
+// buckets (k_chain_join, k_lead_scan).  The regular sequence (PART_ALL) leaves JOIN out: with
+// unskewed scalars both kernels would do nothing, yet each costs ~5 us of the critical path.
+// k_accumulate flags skew, k_bucket_reduce_2 reports it with the terms, and finish_msm then runs
+// JOIN + POST again on the slot (the order of the original sequence; nothing they read was
+// changed by the first reduction).
+constexpr int PART_PREP = 1, PART_SORT = 2, PART_ACC = 4, PART_POST = 8, PART_ALL = 15, PART_JOIN = 16;
 
 // One captured graph of a slot: a contiguous part of the launch sequence for one plan.
 struct Segment {
@@ -358,6 +363,8 @@ uint32_t run_length_for(const MsmDims& d, int n_cu) {
   return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, K));
 }
 
+int finish_plan(const MsmDims& d, const msm_opts* o, int n_cu, Plan* pl);
+
 int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1,
               bool shared = false) {
   *pl = Plan{};
@@ -389,6 +396,12 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   d.nbins = d.W * d.nbc;
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
+  return finish_plan(d, o, n_cu, pl);
+}
+
+// The launch-shape fields that follow from the geometry d.
+int finish_plan(const MsmDims& d, const msm_opts* o, int n_cu, Plan* pl) {
+  const size_t n = d.n;
   pl->d = d;
   pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, n_cu);
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
@@ -566,13 +579,17 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     mark(PH_ACCUM);
   }
   if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc1, s));
-  if (parts & PART_POST) {
+  // profiling mode 1 keeps the joins in line (its per-phase timings include them)
+  const bool joins = (parts & PART_JOIN) || prof;
+  if ((parts & PART_POST) && joins) {
     hipLaunchKernelGGL(k_chain_join, dim3(CJ_GRID), dim3(ACC_THREADS), 0, s, w.skew_list.as<uint32_t>(), total, pl.K,
                        w.g_head.as<uint32_t>(), w.g_hkey.as<uint32_t>(), w.g_tkey.as<uint32_t>(),
                        w.buckets.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.lead_open.as<uint32_t>(),
                        w.lead_flag.as<uint32_t>());
     hipLaunchKernelGGL(k_lead_scan, dim3(1), dim3(LS_THREADS), 0, s, w.lead_val.as<uint32_t>(),
                        w.lead_open.as<uint32_t>(), w.lead_flag.as<uint32_t>(), total, pl.K);
+  }
+  if (parts & PART_POST) {
     mark(PH_FIXUP);
     auto red1 = pl.L == 4    ? k_bucket_reduce_1<4>
                 : pl.L == 9  ? k_bucket_reduce_1<9>
@@ -589,7 +606,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     mark(PH_RED1);
     hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
                        w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
-                       w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total,
+                       w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total, joins ? 1u : 0u,
                        reinterpret_cast<uint32_t*>(sl.h_out_dev));
     mark(PH_RED2);
     mark(PH_READBACK);
@@ -1013,7 +1030,10 @@ int wait_event(hipStream_t s, hipEvent_t e) {
 // milliseconds, and a blocking wait adds a wake-up latency) and take its window terms.  With
 // `terms` the terms are copied out, so the slot can take its next launch before the host tail
 // runs; otherwise the host tail runs here, on the pinned buffer.
-int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr, TailCrew* crew = nullptr) {
+// Wait for the launch in slot `si` and check its flags; its window terms are then in the slot's
+// h_out.  Skewed scalars: the sequence ran without the bucket joins (PART_JOIN), so they and the
+// reduction run again here (the slot's stream is idle: its next launch is enqueued afterwards).
+int wait_slot(DevCtx* c, int si, uint32_t* total_out = nullptr) {
   Slot& sl = c->slot[si];
   const Plan& pl = sl.pl;
   const auto spin_until = clk::now() + std::chrono::milliseconds(50);
@@ -1023,10 +1043,26 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
   HIPCHECK(q);
   const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
   const uint32_t* h = reinterpret_cast<const uint32_t*>(sl.h_out.p);
-  uint32_t err = h[outb / 4];
-  uint32_t total = h[outb / 4 + 1];
+  const uint32_t err = h[outb / 4];
+  if (total_out) *total_out = h[outb / 4 + 1];
+  if (h[outb / 4 + 2]) {
+    if (int rc = enqueue_msm(c, pl, BatchPtrs{}, BatchPtrs{}, si, sl.stream, PART_JOIN | PART_POST, nullptr))
+      return rc;
+    HIPCHECK(hipEventRecord(sl.ev_done, sl.stream));
+    HIPCHECK(hipEventSynchronize(sl.ev_done));
+  }
   if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
   if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
+  return MSM_OK;
+}
+
+int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nullptr, TailCrew* crew = nullptr) {
+  Slot& sl = c->slot[si];
+  const Plan& pl = sl.pl;
+  uint32_t total = 0;
+  if (int rc = wait_slot(c, si, &total)) return rc;
+  const size_t outb = (size_t)pl.d.W * pl.nterms * 32 * 4;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(sl.h_out.p);
   auto t0 = clk::now();
   if (terms)
     terms->assign(h, h + outb / 4);

@@ -345,7 +345,11 @@ constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel 
 // wave (DPP) and across the 16 waves.  Also lists the tiles (FS_CAP entries) of bins too big for
 // k_fine_sort's LDS staging: big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
 constexpr uint32_t BS_THREADS = 1024;
-constexpr uint32_t BS_TILE = 16384;  // 64 KiB of LDS; a two-MSM 2^20 launch has 8,704 bins
+#ifndef MSM_BS_TILE
+#define MSM_BS_TILE 4096
+#endif
+// 16 KiB of LDS per tile (64 KiB measured the same); a two-MSM 2^20 launch has 8,704 bins
+constexpr uint32_t BS_TILE = MSM_BS_TILE;
 extern "C" __global__ void __launch_bounds__(BS_THREADS) k_bin_scan(uint32_t* __restrict__ colsum,
                                                                     uint32_t* __restrict__ bin_base,
                                                                     uint32_t* __restrict__ bin_cur, uint32_t nbins,
@@ -591,14 +595,8 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     if (run) atomicAdd(&cnt[last], run);
   }
   __syncthreads();
-  // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them
-  uint32_t my_cnt[FS_MAXF / FS_THREADS];
-#pragma unroll
-  for (uint32_t q = 0; q < FS_MAXF / FS_THREADS; q++) {
-    const uint32_t f = q * FS_THREADS + threadIdx.x;
-    my_cnt[q] = f < nf ? cnt[f] : 0u;
-  }
-  __syncthreads();
+  // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them (a bucket
+  // ends where the next one starts)
   lds_excl_scan_wave0(cnt, nf);
   __syncthreads();
 #pragma unroll
@@ -606,12 +604,10 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     const uint32_t f = q * FS_THREADS + threadIdx.x;
     if (f < nf) {
       const uint32_t gs = base + cnt[f];
+      const uint32_t ge = base + (f + 1 < nf ? cnt[f + 1] : m);
       bucket_start[key0 + f] = gs;
       if (m > FS_BIG) cursor[key0 + f] = gs;
-      if (my_cnt[q]) {
-        const uint32_t ge = gs + my_cnt[q];
-        for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
-      }
+      for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
     }
   }
   if (m > FS_BIG) return;  // k_big_place moves the entries
@@ -1199,8 +1195,8 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
 // pow2ceil(nchunks)/2 points.
 // Output: X, Y, T, Z in the host's Montgomery form (a * 2^256 mod p, 8 LE words each), written
 // straight into coherent pinned host memory (no readback copy), so the host Horner
-// (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags and the
-// entry count.
+// (hostfield.h) uses them without conversion.  Block 0 also forwards the error flags, the entry
+// count and whether the joins of skewed buckets are still due.
 #ifndef MSM_RED2_THREADS
 #define MSM_RED2_THREADS 512
 #endif
@@ -1217,6 +1213,7 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
                                                                              uint32_t* __restrict__ lead_flag,
                                                                              uint32_t* __restrict__ skew_list,
                                                                              const uint32_t* __restrict__ total,
+                                                                             uint32_t final_pass,
                                                                              uint32_t* __restrict__ out_host) {
   __shared__ uint32_t sh[RED2_THREADS / 2][PT_WORDS];
   const uint32_t w = blockIdx.x / nterms, term = blockIdx.x % nterms;
@@ -1271,12 +1268,19 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
   }
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) {
+      // Without the joins in the sequence (final_pass 0), skewed buckets make the terms invalid:
+      // the host then runs the joins and this reduction again (msm_host.hip PART_JOIN), so the
+      // skew flags stay set for them.
       const size_t tail = (size_t)gridDim.x * 32;
+      const bool skew = skew_list[0] != 0 || *lead_flag != 0;
       out_host[tail] = *err;
       out_host[tail + 1] = *total;
+      out_host[tail + 2] = (skew && !final_pass) ? 1u : 0u;
       *err = 0;  // flags start the next MSM cleared (no memset node in the graph)
-      *lead_flag = 0;
-      skew_list[0] = 0;
+      if (final_pass || !skew) {
+        *lead_flag = 0;
+        skew_list[0] = 0;
+      }
     }
     __threadfence_system();
   }
