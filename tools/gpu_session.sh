@@ -12,6 +12,7 @@
 #   bench        python bench.py (the driver's command)
 #   bench50      50 timed steps, no extras
 #   sizes        pipelined ms per MSM at 2^16..2^19 (20 and 50 steps)
+#   size:LG:LIBS pipelined ms per MSM at 2^LG points for each listed library variant
 #   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
@@ -23,7 +24,8 @@
 #   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
-#                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3)
+#                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3); $BENCH_X adds bench.py
+#                arguments and $KS suffixes the output names
 #   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
 #   latlib:LIBS[:R]  single-MSM latency over in-tree library variants
@@ -31,7 +33,7 @@
 #   set:VAR=VAL / unset:VAR  environment for the steps that follow (e.g. set:MSM_RED_L=8 kstats1)
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 set -u
-[ $# -ge 2 ] || { sed -n 2,32p "$0"; exit 2; }
+[ $# -ge 2 ] || { awk 'NR > 1 && /^#/ { print; next } NR > 1 { exit }' "$0"; exit 2; }
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -68,6 +70,13 @@ for step in "$@"; do
       done ;;
     bench) run bench 300 python bench.py ;;
     bench50) run bench50 300 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" ;;
+    size:*)  # size:LOG2N[:LIBS] -- pipelined ms per MSM at one size for library variants (default libmsm.so)
+      IFS=: read -r _ lg libs <<< "$step"
+      libs=${libs:-libmsm.so}
+      for lib in ${libs//,/ }; do
+        MSM_AMD_LIB=$LIBDIR/$lib run "size${lg}_${lib%.so}" 120 python bench.py --steps 50 --warmup 20 --no-extras \
+          "${BENCH_Q[@]}" --n $((1 << lg))
+      done ;;
     sizes)
       for lg in 16 17 18 19; do
         run size$lg 120 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
@@ -100,7 +109,8 @@ for step in "$@"; do
       IFS=: read -r _ libs rounds <<< "$step"
       for r in $(seq 1 "${rounds:-3}"); do
         for lib in ${libs//,/ }; do
-          MSM_AMD_LIB=$LIBDIR/$lib run "ab_${lib%.so}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          # shellcheck disable=SC2086  # BENCH_X: extra bench.py arguments (set:BENCH_X=...), word-split on purpose
+          MSM_AMD_LIB=$LIBDIR/$lib run "ab_${lib%.so}${KS:-}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}" ${BENCH_X:-}
         done
       done ;;
     env:*)

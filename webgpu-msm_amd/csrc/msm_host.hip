@@ -236,6 +236,7 @@ std::vector<DevCtx*> g_ctx;   // indexed by HIP ordinal
 std::vector<int> g_gfx950;    // HIP ordinals of the gfx950 devices
 int g_nhip = -1;              // HIP devices visible (any architecture)
 std::atomic<int> g_profiling{0};  // read by calls on other devices' threads
+std::atomic<int> g_acc_waves{0};  // k_accumulate waves per SIMD (get_ctx's occupancy query)
 
 int probe_devices() {
   if (g_nhip >= 0) return (int)g_gfx950.size();
@@ -298,6 +299,11 @@ int get_ctx(int device, DevCtx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
       c->n_cu = prop.multiProcessorCount;
+    int acc_blocks = 0;  // k_accumulate workgroups per CU -> waves per SIMD (run_length_for)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&acc_blocks, reinterpret_cast<const void*>(&k_accumulate),
+                                                     ACC_THREADS, 0) == hipSuccess &&
+        acc_blocks > 0)
+      g_acc_waves.store(acc_blocks * (int)(ACC_THREADS / 64) / 4);
     hipSetDevice(prev);
     g_ctx[device] = c;
   }
@@ -347,16 +353,26 @@ uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
   return 16;
 }
 
+// Waves of k_accumulate one SIMD holds (4: VGPR- and LDS-bound), from the runtime's occupancy
+// query at the first device context (g_acc_waves).
+uint64_t acc_waves_per_simd() {
+  const int v = g_acc_waves.load();
+  return v > 0 ? (uint64_t)v : 4u;
+}
+
 // Run length K (entries per k_accumulate lane, a multiple of 4 for the 16-B entry loads): the
-// accumulation holds 4 waves per SIMD (VGPR- and LDS-bound), so its lanes run in rounds of
-// 4 x 4 x CUs waves, and a round only partly filled runs on few SIMDs for a full wave's time.
+// accumulation holds acc_waves_per_simd() waves per SIMD, so its lanes run in rounds of that
+// many x 4 x CUs waves, and a round only partly filled runs on few SIMDs for a full wave's time.
 // So K <= 64 (long enough to amortise the per-run joins) is chosen to fill whole rounds: the
 // fewest rounds r with K <= 64, then the smallest K that fits the launch's entries in r rounds
 // (upper bound: every main-window digit nonzero).  2^20, two MSMs: K = 64, 2 rounds; 2^17, four
-// MSMs: K = 36 (3,868 waves) where K = 32 needed 4,352, a 6% second round.
+// MSMs: K = 36 (3,868 waves) where K = 32 needed 4,352, a 6% second round.  K also bounds how
+// many runs a bucket spans: a bucket over 3 or more whole runs sends the launch through the skew
+// joins (§2.4 of DESIGN.md), so shorter runs than these cost a second reduction on random
+// scalars (a lone 2^20 MSM at K = 44: latency 1.16 -> 1.36 ms).
 uint32_t run_length_for(const MsmDims& d, int n_cu) {
   const uint64_t m = (uint64_t)d.nm * (d.Wm - 1) * d.n;
-  const uint64_t round_lanes = 64ull * 4 * 4 * (uint64_t)(n_cu > 0 ? n_cu : 256);
+  const uint64_t round_lanes = 64ull * acc_waves_per_simd() * 4 * (uint64_t)(n_cu > 0 ? n_cu : 256);
   const uint64_t r = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
   uint64_t K = (m + r * round_lanes - 1) / (r * round_lanes);
   K = (K + 3) & ~3ull;
