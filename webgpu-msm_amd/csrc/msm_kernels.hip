@@ -414,16 +414,17 @@ extern "C" __global__ void __launch_bounds__(BS_THREADS) k_bin_scan(uint32_t* __
 // registers to its slice, with no LDS staging, measured 59 -> 153 us per two-MSM 2^20 launch; the
 // same in k_fine_sort 96 -> 168 us.)
 //
-// Staging keeps 4 B per entry for 16-bit codes: code << 14 | position in the chunk (ch = 2^14),
+// Staging keeps 4 B per entry for 16-bit codes: code << PS_POS | position in the chunk (ch = 2^PS_POS),
 // 64 KiB, so two workgroups share a CU; 32-bit codes (c > 16) stage (code, position) pairs.
+constexpr uint32_t PS_POS = __builtin_ctz(PT_THREADS * PS_R);  // bits of a position in a chunk
 template <typename T>
 struct PartStage;
 template <>
 struct PartStage<uint16_t> {
   using V = uint32_t;
-  static __device__ __forceinline__ V pack(uint32_t code, uint32_t li) { return code << 14 | li; }
-  static __device__ __forceinline__ uint32_t code(V v) { return v >> 14; }
-  static __device__ __forceinline__ uint32_t pos(V v) { return v & 0x3fffu; }
+  static __device__ __forceinline__ V pack(uint32_t code, uint32_t li) { return code << PS_POS | li; }
+  static __device__ __forceinline__ uint32_t code(V v) { return v >> PS_POS; }
+  static __device__ __forceinline__ uint32_t pos(V v) { return v & ((1u << PS_POS) - 1u); }
 };
 template <>
 struct PartStage<uint32_t> {
@@ -432,7 +433,7 @@ struct PartStage<uint32_t> {
   static __device__ __forceinline__ uint32_t code(V v) { return v.x; }
   static __device__ __forceinline__ uint32_t pos(V v) { return v.y; }
 };
-static_assert(PT_THREADS * PS_R == (1u << 14), "PartStage<uint16_t> packs a 14-bit chunk position");
+static_assert(PT_THREADS * PS_R == (1u << PS_POS) && PS_POS <= 16, "PartStage<uint16_t> packs code and position in 32 bits");
 
 template <typename T>
 __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
