@@ -13,6 +13,7 @@
 #   bench50      50 timed steps, no extras
 #   sizes        pipelined ms per MSM at 2^16..2^19 (20 and 50 steps)
 #   size:LG:LIBS pipelined ms per MSM at 2^LG points for each listed library variant
+#   win:LG:C1,C2[:R]  pipelined ms per MSM at 2^LG points over window widths
 #   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
@@ -77,6 +78,14 @@ for step in "$@"; do
         MSM_AMD_LIB=$LIBDIR/$lib run "size${lg}_${lib%.so}" 120 python bench.py --steps 50 --warmup 20 --no-extras \
           "${BENCH_Q[@]}" --n $((1 << lg))
       done ;;
+    win:*)  # win:LG:C1,C2[:R] -- pipelined ms per MSM at 2^LG points over window widths
+      IFS=: read -r _ lg cs rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for cw in ${cs//,/ }; do
+          run "win${lg}_c${cw}_$r" 120 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" \
+            --n $((1 << lg)) --window "$cw"
+        done
+      done ;;
     sizes)
       for lg in 16 17 18 19; do
         run size$lg 120 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
@@ -92,8 +101,10 @@ for step in "$@"; do
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;
     kstats1)
-      MSM_SLOTS=1 MSM_FORK_PREP=0 run kstats1 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats1_d \
-        -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 40 --warmup 10 ;;
+      # shellcheck disable=SC2086
+      MSM_SLOTS=1 MSM_FORK_PREP=0 run "kstats1${KS:-}" 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "gpurun_out/${TAG}_kstats1${KS:-}_d" -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 40 \
+        --warmup 10 ${BENCH_X:-} ;;
     kstats1lib:*)
       IFS=: read -r _ libs <<< "$step"
       for lib in ${libs//,/ }; do
