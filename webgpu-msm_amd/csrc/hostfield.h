@@ -102,34 +102,93 @@ static inline Fq fq_mul(const Fq& a, const Fq& b) {
   }
   return r;
 }
-static inline Fq fq_add(const Fq& a, const Fq& b) {
-  Fq r;
-  u128 c = 0;
+// N independent products r[k] = a[k] b[k], the same CIOS steps interleaved across the N so the
+// core overlaps their carry chains (a lone fq_mul is one long dependent chain: a doubling's
+// four squarings and three products measured as ~9 multiply latencies done one after another).
+template <int N>
+static inline void fq_mul_n(Fq* r, const Fq* a, const Fq* b) {
+  ull t0[N], t1[N], t2[N], t3[N], t4[N];
+#pragma GCC unroll 4
+  for (int k = 0; k < N; k++) t0[k] = t1[k] = t2[k] = t3[k] = t4[k] = 0;
+#pragma GCC unroll 4
   for (int i = 0; i < 4; i++) {
-    c += (u128)a.l[i] + b.l[i];
-    r.l[i] = (uint64_t)c;
-    c >>= 64;
-  }
-  if (geq_p(r.l)) sub_p(r.l);  // p < 2^253: no carry out
-  return r;
-}
-static inline Fq fq_sub(const Fq& a, const Fq& b) {
-  Fq r;
-  u128 borrow = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 t = (u128)a.l[i] - b.l[i] - borrow;
-    r.l[i] = (uint64_t)t;
-    borrow = (t >> 64) ? 1 : 0;
-  }
-  if (borrow) {
-    u128 c = 0;
-    for (int i = 0; i < 4; i++) {
-      c += (u128)r.l[i] + P[i];
-      r.l[i] = (uint64_t)c;
-      c >>= 64;
+#pragma GCC unroll 4
+    for (int k = 0; k < N; k++) {
+      const ull ai = a[k].l[i];
+      ull h0, h1, h2, h3;
+      const ull l0 = mul_lohi(ai, b[k].l[0], &h0), l1 = mul_lohi(ai, b[k].l[1], &h1);
+      const ull l2 = mul_lohi(ai, b[k].l[2], &h2), l3 = mul_lohi(ai, b[k].l[3], &h3);
+      unsigned char c = 0;
+      c = _addcarry_u64(c, t0[k], l0, &t0[k]);
+      c = _addcarry_u64(c, t1[k], l1, &t1[k]);
+      c = _addcarry_u64(c, t2[k], l2, &t2[k]);
+      c = _addcarry_u64(c, t3[k], l3, &t3[k]);
+      c = _addcarry_u64(c, t4[k], 0, &t4[k]);
+      ull t5 = c;
+      c = _addcarry_u64(0, t1[k], h0, &t1[k]);
+      c = _addcarry_u64(c, t2[k], h1, &t2[k]);
+      c = _addcarry_u64(c, t3[k], h2, &t3[k]);
+      c = _addcarry_u64(c, t4[k], h3, &t4[k]);
+      t5 += c;
+      const ull m = t0[k] * NP;
+      const ull m0 = mul_lohi(m, P[0], &h0), m1 = mul_lohi(m, P[1], &h1);
+      const ull m2 = mul_lohi(m, P[2], &h2), m3 = mul_lohi(m, P[3], &h3);
+      ull drop;
+      c = _addcarry_u64(0, t0[k], m0, &drop);
+      c = _addcarry_u64(c, t1[k], m1, &t0[k]);
+      c = _addcarry_u64(c, t2[k], m2, &t1[k]);
+      c = _addcarry_u64(c, t3[k], m3, &t2[k]);
+      c = _addcarry_u64(c, t4[k], 0, &t3[k]);
+      t5 += c;
+      c = _addcarry_u64(0, t0[k], h0, &t0[k]);
+      c = _addcarry_u64(c, t1[k], h1, &t1[k]);
+      c = _addcarry_u64(c, t2[k], h2, &t2[k]);
+      c = _addcarry_u64(c, t3[k], h3, &t3[k]);
+      t4[k] = t5 + c;
     }
   }
-  return r;
+#pragma GCC unroll 4
+  for (int k = 0; k < N; k++) {
+    ull d0, d1, d2, d3;
+    unsigned char br = _subborrow_u64(0, t0[k], P[0], &d0);
+    br = _subborrow_u64(br, t1[k], P[1], &d1);
+    br = _subborrow_u64(br, t2[k], P[2], &d2);
+    br = _subborrow_u64(br, t3[k], P[3], &d3);
+    if (br) {
+      r[k].l[0] = t0[k], r[k].l[1] = t1[k], r[k].l[2] = t2[k], r[k].l[3] = t3[k];
+    } else {
+      r[k].l[0] = d0, r[k].l[1] = d1, r[k].l[2] = d2, r[k].l[3] = d3;
+    }
+  }
+}
+// Branch-free (a data-dependent branch per add mispredicts half the time on random values).
+static inline Fq fq_add(const Fq& a, const Fq& b) {
+  ull s0, s1, s2, s3, d0, d1, d2, d3;
+  unsigned char c = _addcarry_u64(0, a.l[0], b.l[0], &s0);  // p < 2^253: no carry out
+  c = _addcarry_u64(c, a.l[1], b.l[1], &s1);
+  c = _addcarry_u64(c, a.l[2], b.l[2], &s2);
+  _addcarry_u64(c, a.l[3], b.l[3], &s3);
+  unsigned char br = _subborrow_u64(0, s0, P[0], &d0);
+  br = _subborrow_u64(br, s1, P[1], &d1);
+  br = _subborrow_u64(br, s2, P[2], &d2);
+  br = _subborrow_u64(br, s3, P[3], &d3);
+  const ull keep = 0ull - (ull)br;  // all ones when a + b < p
+  return Fq{{(s0 & keep) | (d0 & ~keep), (s1 & keep) | (d1 & ~keep), (s2 & keep) | (d2 & ~keep),
+             (s3 & keep) | (d3 & ~keep)}};
+}
+static inline Fq fq_sub(const Fq& a, const Fq& b) {
+  ull d0, d1, d2, d3;
+  unsigned char br = _subborrow_u64(0, a.l[0], b.l[0], &d0);
+  br = _subborrow_u64(br, a.l[1], b.l[1], &d1);
+  br = _subborrow_u64(br, a.l[2], b.l[2], &d2);
+  br = _subborrow_u64(br, a.l[3], b.l[3], &d3);
+  const ull m = 0ull - (ull)br;  // add p back when a < b
+  ull r0, r1, r2, r3;
+  unsigned char c = _addcarry_u64(0, d0, P[0] & m, &r0);
+  c = _addcarry_u64(c, d1, P[1] & m, &r1);
+  c = _addcarry_u64(c, d2, P[2] & m, &r2);
+  _addcarry_u64(c, d3, P[3] & m, &r3);
+  return Fq{{r0, r1, r2, r3}};
 }
 static inline Fq fq_zero() { return Fq{{0, 0, 0, 0}}; }
 static inline Fq fq_one() { return Fq{{RMODP[0], RMODP[1], RMODP[2], RMODP[3]}}; }
@@ -156,10 +215,74 @@ static inline Fq fq_pow(const Fq& a, const uint64_t e[4]) {
     }
   return r;
 }
-static inline Fq fq_inv(const Fq& a) {
+static inline Fq fq_inv_pow(const Fq& a) {
   const uint64_t E[4] = {0x0a117fffffffffffULL, 0x59aa76fed0000001ULL, 0x60b44d1e5c37b001ULL,
                          0x12ab655e9a2ca556ULL};  // p - 2
   return fq_pow(a, E);
+}
+
+static const uint64_t R3MODP[4] = {0x6a4295c90f65454cULL, 0x624d23ffae271699ULL, 0xb1e55ef6f1c9d713ULL,
+                                   0x0601dfa555c48ddaULL};  // R^3 mod p
+// x <- x / 2^k mod p for x < p, 1 <= k <= 63: add the multiple of p that clears the low k bits
+// (m = x * (-p^-1) mod 2^k), shift; (x + m p) / 2^k < 2p, so one conditional subtraction.
+static inline void div2k_mod(uint64_t x[4], int k) {
+  const ull m = (x[0] * NP) & ((1ull << k) - 1);
+  ull t[5];
+  u128 acc = 0;
+  for (int i = 0; i < 4; i++) {
+    acc += (u128)m * P[i] + x[i];
+    t[i] = (ull)acc;
+    acc >>= 64;
+  }
+  t[4] = (ull)acc;
+  for (int i = 0; i < 4; i++) x[i] = (t[i] >> k) | (t[i + 1] << (64 - k));
+  if (geq_p(x)) sub_p(x);
+}
+// u >>= ctz(u) (u odd afterwards, u != 0); x <- x / 2^ctz(u) mod p alongside.
+static inline void strip_twos(ull u[4], uint64_t x[4]) {
+  while (!(u[0] & 1)) {
+    const int k = u[0] ? __builtin_ctzll(u[0]) : 63;
+    for (int i = 0; i < 3; i++) u[i] = (u[i] >> k) | (u[i + 1] << (64 - k));
+    u[3] >>= k;
+    div2k_mod(x, k);
+  }
+}
+static inline bool u4_is_one(const ull u[4]) { return u[0] == 1 && !(u[1] | u[2] | u[3]); }
+static inline bool u4_geq(const ull a[4], const ull b[4]) {
+  for (int i = 3; i >= 0; i--)
+    if (a[i] != b[i]) return a[i] > b[i];
+  return true;
+}
+static inline void u4_sub(ull a[4], const ull b[4]) {
+  unsigned char br = _subborrow_u64(0, a[0], b[0], &a[0]);
+  br = _subborrow_u64(br, a[1], b[1], &a[1]);
+  br = _subborrow_u64(br, a[2], b[2], &a[2]);
+  _subborrow_u64(br, a[3], b[3], &a[3]);
+}
+// Inverse by the binary extended Euclidean algorithm on the Montgomery representative a' = aR:
+// invariants x1 a' = u, x2 a' = v (mod p) with u, v odd; the smaller is subtracted from the larger
+// and its factors of two stripped (several bits per step through div2k_mod).  x = a'^-1 when u
+// or v reaches 1, and x R^3 / R = a^-1 R is the Montgomery form of the inverse.  Variable time
+// (nothing here is secret); ~4x faster than a^(p-2) (253 dependent squarings).  0 -> 0.
+static inline Fq fq_inv(const Fq& a) {
+  if (!(a.l[0] | a.l[1] | a.l[2] | a.l[3])) return a;
+  ull u[4] = {a.l[0], a.l[1], a.l[2], a.l[3]}, v[4] = {P[0], P[1], P[2], P[3]};
+  Fq x1 = {{1, 0, 0, 0}}, x2 = {{0, 0, 0, 0}};
+  strip_twos(u, x1.l);
+  const Fq r3 = {{R3MODP[0], R3MODP[1], R3MODP[2], R3MODP[3]}};
+  for (;;) {
+    if (u4_is_one(u)) return fq_mul(x1, r3);
+    if (u4_geq(u, v)) {
+      u4_sub(u, v);
+      x1 = fq_sub(x1, x2);
+      strip_twos(u, x1.l);
+    } else {
+      u4_sub(v, u);
+      x2 = fq_sub(x2, x1);
+      strip_twos(v, x2.l);
+      if (u4_is_one(v)) return fq_mul(x2, r3);
+    }
+  }
 }
 
 // 8 big-endian u32 words (bytes.rs layout) <-> standard limbs
@@ -185,13 +308,24 @@ static inline Pt pt_identity() { return Pt{fq_zero(), fq_one(), fq_zero(), fq_on
 // p + q; with want_t = false the result's T is left stale (fine when a doubling comes next:
 // dbl-2008-hwcd never reads T).
 static inline Pt pt_add(const Pt& p, const Pt& q, bool want_t = true) {
-  Fq A = fq_mul(fq_sub(p.Y, p.X), fq_sub(q.Y, q.X));
-  Fq B = fq_mul(fq_add(p.Y, p.X), fq_add(q.Y, q.X));
-  Fq C = fq_mul(fq_mul(p.T, q.T), Fq{{K2D_M[0], K2D_M[1], K2D_M[2], K2D_M[3]}});
-  Fq D = fq_mul(p.Z, q.Z);
-  D = fq_add(D, D);
-  Fq E = fq_sub(B, A), F = fq_sub(D, C), G = fq_add(D, C), H = fq_add(B, A);
-  return Pt{fq_mul(E, F), fq_mul(G, H), want_t ? fq_mul(E, H) : fq_zero(), fq_mul(F, G)};
+  const Fq a1[4] = {fq_sub(p.Y, p.X), fq_add(p.Y, p.X), p.T, p.Z};
+  const Fq b1[4] = {fq_sub(q.Y, q.X), fq_add(q.Y, q.X), q.T, q.Z};
+  Fq m1[4];
+  fq_mul_n<4>(m1, a1, b1);  // A, B, T1 T2, Z1 Z2
+  const Fq& A = m1[0];
+  const Fq& B = m1[1];
+  const Fq C = fq_mul(m1[2], Fq{{K2D_M[0], K2D_M[1], K2D_M[2], K2D_M[3]}});
+  const Fq D = fq_add(m1[3], m1[3]);
+  const Fq E = fq_sub(B, A), F = fq_sub(D, C), G = fq_add(D, C), H = fq_add(B, A);
+  const Fq a2[4] = {E, G, F, E}, b2[4] = {F, H, G, H};
+  Fq m2[4];
+  if (want_t) {
+    fq_mul_n<4>(m2, a2, b2);
+  } else {
+    fq_mul_n<3>(m2, a2, b2);
+    m2[3] = fq_zero();
+  }
+  return Pt{m2[0], m2[1], m2[3], m2[2]};
 }
 static inline Pt pt_dbl(const Pt& p) {
   Fq A = fq_mul(p.X, p.X);
@@ -206,23 +340,31 @@ static inline Pt pt_dbl(const Pt& p) {
   Fq H = fq_sub(fq_zero(), fq_add(A, B));
   return Pt{fq_mul(E, F), fq_mul(G, H), fq_mul(E, H), fq_mul(F, G)};
 }
-// 2^k * p.  dbl-2008-hwcd never reads T, so every doubling but the last skips T3 = E*H.
+// 2^k * p.  dbl-2008-hwcd never reads T, so every doubling but the last skips T3 = E*H.  The
+// four squarings, then the output products, run as interleaved batches (fq_mul_n).
 static inline Pt pt_dbl_n(Pt p, int k) {
   for (int i = 0; i < k; i++) {
-    Fq A = fq_mul(p.X, p.X);
-    Fq B = fq_mul(p.Y, p.Y);
-    Fq C = fq_mul(p.Z, p.Z);
-    C = fq_add(C, C);
-    Fq S = fq_add(p.X, p.Y);
-    S = fq_mul(S, S);
-    Fq E = fq_sub(fq_sub(S, A), B);
-    Fq G = fq_sub(B, A);
-    Fq F = fq_sub(G, C);
-    Fq H = fq_sub(fq_zero(), fq_add(A, B));
-    p.X = fq_mul(E, F);
-    p.Y = fq_mul(G, H);
-    p.Z = fq_mul(F, G);
-    if (i == k - 1) p.T = fq_mul(E, H);
+    const Fq S0 = fq_add(p.X, p.Y);
+    const Fq in[4] = {p.X, p.Y, p.Z, S0};
+    Fq sq[4];
+    fq_mul_n<4>(sq, in, in);
+    const Fq &A = sq[0], &B = sq[1], &S = sq[3];
+    const Fq C = fq_add(sq[2], sq[2]);
+    const Fq E = fq_sub(fq_sub(S, A), B);
+    const Fq G = fq_sub(B, A);
+    const Fq F = fq_sub(G, C);
+    const Fq H = fq_sub(fq_zero(), fq_add(A, B));
+    const Fq ma[4] = {E, G, F, E}, mb[4] = {F, H, G, H};
+    Fq out[4];
+    if (i == k - 1) {
+      fq_mul_n<4>(out, ma, mb);
+      p.T = out[3];
+    } else {
+      fq_mul_n<3>(out, ma, mb);
+    }
+    p.X = out[0];
+    p.Y = out[1];
+    p.Z = out[2];
   }
   return p;
 }

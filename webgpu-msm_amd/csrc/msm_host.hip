@@ -2111,6 +2111,48 @@ int msm_test_tail(size_t n, const uint32_t* terms, int helpers, uint32_t out_xy_
   return MSM_OK;
 }
 
+// Host field / curve timings (ns per operation, dependent chains): what 0 = fq_mul, 1 = one
+// doubling of pt_dbl_n, 2 = pt_add, 3 = fq_inv.  For sizing the host tail.
+int msm_test_host_timing(int what, size_t iters, double* ns) {
+  if (!ns || iters == 0 || what < 0 || what > 4) return MSM_ERR_INVALID_ARG;
+  if (what == 4) {  // self-check: binary-Euclid fq_inv against a^(p-2) on iters pseudo-random a
+    uint64_t st = 0x9E3779B97F4A7C15ull, bad = 0;
+    for (size_t i = 0; i < iters; i++) {
+      uint64_t s[4];
+      for (int j = 0; j < 4; j++) {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        s[j] = st ^ (st >> 29);
+      }
+      s[3] &= (i & 1) ? 0x0fffffffffffffffull : 0x000000000000ffffull;  // full-width and short
+      if (i == 0) s[0] = 1, s[1] = s[2] = s[3] = 0;
+      if (i == 1) s[0] = P[0] - 1, s[1] = P[1], s[2] = P[2], s[3] = P[3];
+      const Fq a = fq_from_std(s);
+      const Fq x = fq_inv(a);
+      bad += !fq_eq(x, fq_inv_pow(a)) || !fq_eq(fq_mul(x, a), fq_one());
+    }
+    bad += !fq_is_zero(fq_inv(fq_zero()));
+    *ns = (double)bad;
+    return MSM_OK;
+  }
+  Pt p = pt_identity();
+  p.X = fq_one();
+  p.Y = fq_add(fq_one(), fq_one());
+  p.T = fq_add(p.Y, fq_one());
+  p.Z = fq_add(p.T, fq_one());
+  Fq a = p.Z;
+  const auto t0 = clk::now();
+  for (size_t i = 0; i < iters; i++) {
+    if (what == 0) a = fq_mul(a, a);
+    else if (what == 1) p = pt_dbl_n(p, 1);
+    else if (what == 2) p = pt_add(p, p);
+    else a = fq_inv(a);
+  }
+  *ns = std::chrono::duration<double, std::nano>(clk::now() - t0).count() / (double)iters;
+  volatile uint64_t sink = a.l[0] ^ p.X.l[0];
+  (void)sink;
+  return MSM_OK;
+}
+
 // The number of window-term words msm_test_tail reads for n points.
 size_t msm_test_tail_words(size_t n) {
   Plan pl;

@@ -127,8 +127,11 @@ def load() -> ctypes.CDLL:
                               u32p], ctypes.c_int),
         "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_tail_words": ([sz], sz),
+        "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
+        if name.startswith("msm_test_") and not hasattr(L, name):
+            continue  # a test hook an older library variant (MSM_AMD_LIB A/B builds) predates
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
