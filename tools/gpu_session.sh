@@ -13,6 +13,7 @@
 #   bench50      50 timed steps, no extras
 #   sizes        pipelined ms per MSM at 2^16..2^19 (20 and 50 steps)
 #   size:LG:LIBS pipelined ms per MSM at 2^LG points for each listed library variant
+#   steps:K1,K2[:R]  the 2^20 bench over timed step counts
 #   win:LG:C1,C2[:R]  pipelined ms per MSM at 2^LG points over window widths
 #   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
@@ -60,7 +61,7 @@ PYTEST=(python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method th
 
 for step in "$@"; do
   case $step in
-    tests) run tests 900 "${PYTEST[@]}" ;;
+    tests) run "tests${KS:-}" 900 "${PYTEST[@]}" ;;
     tests_alt)
       MSM_NO_GRAPH=1 run tests_eager 900 "${PYTEST[@]}" -k "not random_sweep"
       MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 "${PYTEST[@]}" -k "not random_sweep" ;;
@@ -71,11 +72,18 @@ for step in "$@"; do
       done ;;
     bench) run bench 300 python bench.py ;;
     bench50) run bench50 300 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" ;;
+    steps:*)  # steps:K1,K2[:R] -- 2^20 bench over timed step counts (pipeline fill / drain share)
+      IFS=: read -r _ ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "steps${k}_$r" 300 python bench.py --steps "$k" --warmup 10 --no-extras "${BENCH_Q[@]}"
+        done
+      done ;;
     size:*)  # size:LOG2N[:LIBS] -- pipelined ms per MSM at one size for library variants (default libmsm.so)
       IFS=: read -r _ lg libs <<< "$step"
       libs=${libs:-libmsm.so}
       for lib in ${libs//,/ }; do
-        MSM_AMD_LIB=$LIBDIR/$lib run "size${lg}_${lib%.so}" 120 python bench.py --steps 50 --warmup 20 --no-extras \
+        MSM_AMD_LIB=$LIBDIR/$lib run "size${lg}_${lib%.so}${KS:-}" 120 python bench.py --steps 50 --warmup 20 --no-extras \
           "${BENCH_Q[@]}" --n $((1 << lg))
       done ;;
     win:*)  # win:LG:C1,C2[:R] -- pipelined ms per MSM at 2^LG points over window widths
