@@ -1288,14 +1288,16 @@ int pipeline_slots(size_t n, const msm_opts* o) {
 // 2^18 0.420 -> 0.381, 2^19 0.679 -> 0.638, 2^20 1.162 -> 1.136.  Four per launch up to 2^18,
 // measured once the reduction kept one wave per SIMD and two launches are in flight
 // (profiles/r2mn_*, r2y_*): 2^17 0.268 -> 0.248, 2^18 0.363 -> 0.347 ms per MSM; 2^19 +1.5%,
-// 2^20 +4.5% (kept at two).  Eight up to 2^16 (profiles/r2bg_batch8_ab.txt: 2^16 0.132 -> 0.126,
-// 2^17 within 1%), when the count fills eight-MSM launches without a mostly padded last one.
+// 2^20 +4.5% (kept at two).  Eight up to 2^16: a four-MSM 2^16 launch costs ~0.64 ms of pipeline
+// time and an eight-MSM one ~1.04 (profiles/r3/batch_sizes.txt: 0.13 against 0.16 ms per MSM over
+// 50 MSMs, the last launch padded; 2^17 and 2^18 are 2-13% slower with eight), so eight is taken
+// whenever its launches, padded last one included, cost less: ceil(count/8) * 13 < ceil(count/4) * 8.
 // MSM_BATCH overrides (1..MSM_MAX_BATCH).
 uint32_t pipeline_batch(size_t n, size_t count) {
   static const int env = getenv("MSM_BATCH") ? atoi(getenv("MSM_BATCH")) : 0;
   uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH)
                          : (n <= (1u << 18) ? 4u : n <= (1u << 20) ? 2u : 1u);
-  if (env < 1 && n <= (1u << 16) && count >= 8 && (count % 8 == 0 || count % 8 > 4)) nm = 8;
+  if (env < 1 && n <= (1u << 16) && count >= 8 && (count + 7) / 8 * 13 < (count + 3) / 4 * 8) nm = 8;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
