@@ -46,18 +46,31 @@ const expect = xArg ? { x: BigInt(xArg), y: BigInt(yArg) } : null;
     flattenU32(points, scalars);
     flat.push(performance.now() - t0);
   }
-  // the same MSM from flat wire buffers (no marshalling): the addon + libmsm share
-  const flatTimes = [];
-  for (let r = 0; r <= runs; r++) {
-    const t0 = performance.now();
-    const res = await compute_msm(pw, sw);
-    const t1 = performance.now();
-    if (r > 0) flatTimes.push(t1 - t0);
-    if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
-  }
+  // the same MSM from flat wire buffers (no marshalling): the addon + libmsm share.  Over a
+  // SharedArrayBuffer (as the reference allocates its buffers, submission.ts:35-39) the addon reads
+  // them in place; over a plain ArrayBuffer (pw, sw) it copies them first (detachable memory).
+  const share = (a) => {
+    const b = new Uint32Array(new SharedArrayBuffer(a.length * 4));
+    b.set(a);
+    return b;
+  };
+  const spw = share(pw), ssw = share(sw);
+  const timeFlat = async (p, s) => {
+    const ts = [];
+    for (let r = 0; r <= runs; r++) {
+      const t0 = performance.now();
+      const res = await compute_msm(p, s);
+      const t1 = performance.now();
+      if (r > 0) ts.push(t1 - t0);
+      if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
+    }
+    return ts;
+  };
+  const flatTimes = await timeFlat(spw, ssw);
+  const copyTimes = await timeFlat(pw, sw);
   const med = (xs) => [...xs].sort((a, b) => a - b)[Math.floor(xs.length / 2)];
   console.log(JSON.stringify({ node_e2e_ms: med(times), marshal_ms: med(flat), flat_input_ms: med(flatTimes),
-                               runs_ms: times, correct: expect ? ok : null }));
+                               flat_copied_input_ms: med(copyTimes), runs_ms: times, correct: expect ? ok : null }));
 })().catch((e) => {
   console.log(JSON.stringify({ error: String(e) }));
   process.exit(1);
