@@ -236,6 +236,25 @@ def test_eight_msms_per_launch_small_sizes():
     assert [as_xy(r) for r in out] == exps[:13]
 
 
+@pytest.mark.parametrize("count,per", [(18, 8), (12, 4)])
+def test_small_size_batch_choice(count, per):
+    # up to 2^16, eight per launch whenever its launches (the padded last one included) cost less
+    # than four per launch: 18 MSMs -> 3 launches of eight (2 real in the last), 12 -> 3 of four
+    n = 1 << 16
+    d_pts = _dev(M.gen_points(n))
+    scs = [M.gen_scalars(n, seed=1500 + j) for j in range(count)]
+    exps = [closed_form(1, 1, s) for s in scs]
+    M.set_profiling(2)
+    try:
+        out = M.compute_msm_many_device([d_pts] * count, [_dev(s) for s in scs], n, flags=M.MSM_FLAG_SERIAL)
+        prof = M.last_profile()
+    finally:
+        M.set_profiling(False)
+    assert [as_xy(r) for r in out] == exps
+    if "MSM_BATCH" not in os.environ:
+        assert prof["msms_per_launch"] == per and prof["profiled"] == -(-count // per)
+
+
 def test_beyond_2_20_all_entries():
     # 2^21 + 17 points: one MSM per launch in the pipelined plan, L = 8 reduction for a lone MSM,
     # the host path as 16 slices, the last short and padded; device, pipelined and host entries agree with
