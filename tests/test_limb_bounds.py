@@ -164,7 +164,7 @@ def fe_sub(a: B, b: B) -> B:
     return fe_norm(fe_sub_u(a, b))
 
 
-def fe_neg_v(b: B) -> B:  # pre_neg_if's unnormalised 5p - kt
+def fe_neg_v(b: B) -> B:  # kt_neg_if's unnormalised 5p - kt
     for i in range(NL):
         assert K5P29[i] >= b.l[i]
     assert b.v <= 2 * P  # B.v is an exclusive bound
@@ -380,7 +380,7 @@ REVIEWED = {
     ("ec.cuh", "pt_madd"): "9b3453a645881673",
     ("ec.cuh", "pt_add"): "1449f0a88822c610",
     ("ec.cuh", "pt_dbl"): "784353f9934ef437",
-    ("ec.cuh", "pre_neg_if"): "aa8719a3c1144d3b",
+    ("ec.cuh", "kt_neg_if"): "19c79f3cf45dee09",
     ("ec.cuh", "pt_add_quad"): "875eba21c1f11e82",
 }
 

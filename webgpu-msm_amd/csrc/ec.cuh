@@ -39,7 +39,7 @@ __device__ __forceinline__ xyzt pt_identity() {
 __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
   fe A = fe_mul(fe_sub_v(p.Y, p.X), q.ymx);  // V*N
   fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);    // S*N
-  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*V for a negated q, pre_neg_if)
+  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*V for a negated q, kt_neg_if)
   fe E = fe_sub_v(B, A);                     // V
   fe F = fe_sub_v(p.Z, C);                   // V
   fe G = fe_add(p.Z, C);                     // S
@@ -90,14 +90,13 @@ __device__ __forceinline__ xyzt pt_dbl(const xyzt& p) {
   return r;
 }
 
-// -q = (-x, y): swap (y - x, y + x)/2 and negate d*t.  The negated kt = 5p - kt is left
-// unnormalised (V form), legal as pt_madd's C = T * kt operand (N * V).
-__device__ __forceinline__ pre pre_neg_if(const pre& q, bool neg) {
-  pre r;
-  r.ymx = fe_sel(neg, q.ymx, q.ypx);
-  r.ypx = fe_sel(neg, q.ypx, q.ymx);
+// d*t of -q = (-x, y) is -d*t: 5p - kt, left unnormalised (V form), legal as pt_madd's
+// C = T * kt operand (N * V).  (The other half of the negation, swapping (y-x)/2 and (y+x)/2,
+// is done by the record gather: msm_kernels.hip load_pre_signed.)
+__device__ __forceinline__ fe kt_neg_if(const fe& kt, bool neg) {
+  fe r;
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.kt.v[i] = neg ? K5P29[i] - q.kt.v[i] : q.kt.v[i];
+  for (int i = 0; i < NL; i++) r.v[i] = neg ? K5P29[i] - kt.v[i] : kt.v[i];
   return r;
 }
 

@@ -132,15 +132,17 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
   }
   fe ymx = fe_sub(y, x);
   fe ypx = fe_add_n(y, x);
-  uint32_t rec[32];
+  uint32_t rec[32];  // layout: msm_dev.h PRE_WORDS
+#pragma unroll
+  for (int k = 0; k < 32; k++) rec[k] = 0;
 #pragma unroll
   for (int k = 0; k < NL; k++) {
     rec[k] = ymx.v[k];
-    rec[NL + k] = ypx.v[k];
-    rec[2 * NL + k] = kt.v[k];
+    rec[PRE_HALF + k] = ypx.v[k];
   }
 #pragma unroll
-  for (int k = 3 * NL; k < 32; k++) rec[k] = 0;
+  for (int k = 0; k < NL - 1; k++) rec[PRE_KT + k] = kt.v[k];
+  rec[NL] = rec[PRE_HALF + NL] = kt.v[NL - 1];  // in both halves: read from whichever comes first
 #pragma unroll
   for (uint32_t q = 0; q < 8; q++)
     st[pp_slot(i, q)] = make_uint4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
@@ -175,21 +177,34 @@ extern "C" __global__ void __launch_bounds__(256) k_pad_identity(uint32_t* __res
   }
 }
 
-__device__ __forceinline__ pre load_pre(const uint32_t* __restrict__ pts, uint32_t idx) {
-  const uint4* src = reinterpret_cast<const uint4*>(pts + (size_t)idx * 32);
-  uint32_t rec[28];
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    uint4 v = src[k];
-    rec[4 * k] = v.x; rec[4 * k + 1] = v.y; rec[4 * k + 2] = v.z; rec[4 * k + 3] = v.w;
-  }
+// Gathers the record of sorted entry `ent` (point index << 1 | sign) as the point it adds:
+// a negated point's (y-x)/2 and (y+x)/2 swap by reading the record's halves in the other order
+// (msm_dev.h PRE_WORDS), and its d*t is negated (kt_neg_if).
+__device__ __forceinline__ pre load_pre_signed(const uint32_t* __restrict__ pts, uint32_t ent) {
+  const uint32_t sgn = ent & 1u;
+  const bool neg = sgn != 0;
+  // byte offsets: record (ent >> 1) * 128 = (ent & ~1) * 64; halves at 48 sgn and 48 (1 - sgn)
+  const char* rec = reinterpret_cast<const char*>(pts) + ((size_t)(ent & ~1u) << 6);
+  const uint32_t o0 = sgn * (PRE_HALF * 4);
+  const uint32_t* h0 = reinterpret_cast<const uint32_t*>(rec + o0);
+  const uint32_t* h1 = reinterpret_cast<const uint32_t*>(rec + (o0 ^ (PRE_HALF * 4)));
+  const uint4 a0 = reinterpret_cast<const uint4*>(h0)[0], a1 = reinterpret_cast<const uint4*>(h0)[1];
+  const uint2 a2 = reinterpret_cast<const uint2*>(h0)[4];
+  const uint4 b0 = reinterpret_cast<const uint4*>(h1)[0], b1 = reinterpret_cast<const uint4*>(h1)[1];
+  const uint32_t b2 = h1[8];
+  const uint4 c0 = reinterpret_cast<const uint4*>(rec + PRE_KT * 4)[0];
+  const uint4 c1 = reinterpret_cast<const uint4*>(rec + PRE_KT * 4)[1];
+  const uint32_t av[NL] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x};
+  const uint32_t bv[NL] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2};
+  const uint32_t kv[NL] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, a2.y};
   pre q;
 #pragma unroll
   for (int k = 0; k < NL; k++) {
-    q.ymx.v[k] = rec[k];
-    q.ypx.v[k] = rec[NL + k];
-    q.kt.v[k] = rec[2 * NL + k];
+    q.ymx.v[k] = av[k];
+    q.ypx.v[k] = bv[k];
+    q.kt.v[k] = kv[k];
   }
+  q.kt = kt_neg_if(q.kt, neg);
   return q;
 }
 
@@ -859,7 +874,7 @@ __device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WOR
 #else
       const uint32_t ent = sorted_entry[pos];
 #endif
-      pre q = pre_neg_if(load_pre(pts, ent >> 1), (ent & 1u) != 0);
+      const pre q = load_pre_signed(pts, ent);
       acc = pt_madd(acc, q);
     }
     cont = bend > e;  // bucket `cur` continues into the next run
