@@ -176,26 +176,183 @@ PT = dict(X=N_MUL, Y=N_MUL, T=N_MUL, Z=N_MUL)
 ONE29 = 536870474 + (276299775 << 29)  # value of Montgomery one is < p; covered by N_MUL
 
 
+# ---- signed differences (fp29.cuh fe_sub_s / fe_mul_sd, pt_madd) ----------------------------------
+DELTA_SD_LOG = 26  # fp29.cuh: the bias DELTA_SD p 2^232 added through the seeds of columns 8..16
+SD_OFF58 = [-1, -3, -3, -5, -9, -9, -12, -14, -14, -12, -11, -9, -6, -5, -2, -1, -1, 0]  # fp29.cuh: O_k / 2^58
+
+
+def sd_seed(wide: int, k: int) -> int:
+    """fp29.cuh fe_mul_sd_seed as a signed integer: register offset + bias + O_k - O_(k-1) / 2^29."""
+    bias = (P29[k - (NL - 1)] << DELTA_SD_LOG) if NL - 1 <= k < 2 * NL - 1 else 0
+    return (seed(wide, k) if k <= NL else 0) + bias + (SD_OFF58[k] << 58) - ((SD_OFF58[k - 1] << 29) if k >= 1 else 0)
+
+
+class SB:
+    """Interval bounds of a field element with signed limbs: per-limb [lo, hi] and value [vlo, vhi]
+    (all inclusive)."""
+
+    def __init__(self, lo, hi, vlo, vhi):
+        self.lo, self.hi, self.vlo, self.vhi = list(lo), list(hi), vlo, vhi
+
+    @staticmethod
+    def of(b: B) -> "SB":  # an unsigned form (exclusive value bound b.v)
+        return SB([0] * NL, list(b.l), 0, b.v - 1)
+
+
+def sb_add(a: SB, b: SB) -> SB:
+    return SB([x + y for x, y in zip(a.lo, b.lo)], [x + y for x, y in zip(a.hi, b.hi)], a.vlo + b.vlo, a.vhi + b.vhi)
+
+
+def fe_sub_s(a: SB, b: SB) -> SB:
+    return SB([x - y for x, y in zip(a.lo, b.hi)], [x - y for x, y in zip(a.hi, b.lo)], a.vlo - b.vhi, a.vhi - b.vlo)
+
+
+def _ival_mul(a0, a1, b0, b1):
+    c = (a0 * b0, a0 * b1, a1 * b0, a1 * b1)
+    return min(c), max(c)
+
+
+def fe_mul_sd(a: SB, b: SB, wide: int = WIDE_ALL) -> B:
+    """fp29.cuh fe_mul_sd: signed 32x32 products, signed carries, result biased by DELTA_SD p / 2^29.
+    Asserts every operand limb fits an int32, every column register fits an int64, and the result
+    lies in [0, 2p) -- i.e. it is an ordinary fe_mul output (N_MUL)."""
+    for x in a.lo + b.lo:
+        assert x >= -(1 << 31)
+    for x in a.hi + b.hi:
+        assert x < 1 << 31
+    delta = 1 << DELTA_SD_LOG
+    bias = [delta * P29[k - (NL - 1)] if NL - 1 <= k < 2 * NL - 1 else 0 for k in range(2 * NL)]
+    lo, hi = [0] * (2 * NL), [0] * (2 * NL)
+    for i in range(NL):
+        for j in range(NL):
+            x0, x1 = _ival_mul(a.lo[i], a.hi[i], b.lo[j], b.hi[j])
+            lo[i + j] += x0
+            hi[i + j] += x1
+    clo = chi = 0
+    for k in range(2 * NL):
+        red = sum(digit_max(wide, i) * P29[k - i] for i in range(NL) if 1 <= k - i < NL)
+        col_lo = lo[k] + bias[k] + clo
+        col_hi = hi[k] + bias[k] + red + chi
+        off = seed(wide, k) if k <= NL else 0  # register offset (2^32 - 1, -7), then the centring offset O_k
+        o = SD_OFF58[k] << 58
+        assert -(1 << 63) <= col_lo + min(0, off) + o and col_hi + max(0, off) + o < 1 << 63, \
+            f"column {k} leaves int64"
+        if k < NL:  # (column + digit) / 2^29, floor
+            clo, chi = col_lo >> LB, (col_hi + digit_max(wide, k)) >> LB
+        else:
+            clo, chi = col_lo >> LB, col_hi >> LB
+    t0, t1 = _ival_mul(a.vlo, a.vhi, b.vlo, b.vhi)
+    extra = sum(digit_max(wide, i) << (LB * i) for i in range(NL)) * P
+    X = delta * P << (LB * (NL - 1))
+    assert t0 + X >= 0, "fe_mul_sd result may be negative"
+    assert t1 + X + extra < 2 * P * R, "fe_mul_sd result may reach 2p"
+    return N_MUL
+
+
 def test_madd_bounds():
     # halved record from k_prepare_points: ymx = fe_sub (normalised), ypx = fe_add_n, kt = fe_mul
     ymx = fe_sub(N_MUL, N_MUL)
     ypx = fe_norm(fe_add(N_MUL, N_MUL))
     kt = N_MUL
     for neg in (False, True):
+        # the gather swaps the halves of a negated point (load_pre_signed); kt_neg_if negates d t
         q_ymx, q_ypx = (ypx, ymx) if neg else (ymx, ypx)
         q_kt = fe_neg_v(kt) if neg else kt
-        p = PT
-        A = fe_mul(fe_sub_v(p["Y"], p["X"]), q_ymx)
-        Bv = fe_mul(fe_add(p["Y"], p["X"]), q_ypx)
-        C = fe_mul(p["T"], q_kt)
-        E = fe_sub_v(Bv, A)
-        F = fe_sub_v(p["Z"], C)
-        G = fe_add(p["Z"], C)
+        X = Y = T = Z = SB.of(N_MUL)
+        A = fe_mul_sd(fe_sub_s(Y, X), SB.of(q_ymx))
+        Bv = fe_mul(fe_add(N_MUL, N_MUL), q_ypx)
+        C = fe_mul(N_MUL, q_kt)
+        E = fe_sub_s(SB.of(Bv), SB.of(A))
+        F = fe_sub_s(Z, SB.of(C))
+        G = fe_add(N_MUL, C)
         H = fe_add(Bv, A)
-        fe_mul(E, F, WIDE_EF)
+        fe_mul_sd(E, F)
         fe_mul(G, H)
-        fe_mul(E, H)
-        fe_mul(F, G)
+        fe_mul_sd(E, SB.of(H))
+        fe_mul_sd(F, SB.of(G))
+
+
+def fe_mul_sd_exact(a, b, wide: int = WIDE_ALL):
+    """Bit-exact model of fp29.cuh fe_mul_sd on limb lists (signed limbs; 64-bit two's-complement
+    registers, wrap checked against the true integers): returns the 9 output limbs."""
+    M64 = (1 << 64) - 1
+
+    def s64(x):
+        x &= M64
+        return x - (1 << 64) if x >> 63 else x
+
+    def s32(x):
+        x &= 0xFFFFFFFF
+        return x - (1 << 32) if x >> 31 else x
+
+    c = [sd_seed(wide, k) for k in range(2 * NL)]  # the registers, as signed integers
+    for i in range(NL):
+        for j in range(NL):
+            c[i + j] += s32(a[i]) * s32(b[j])
+    for i in range(NL):
+        assert -(1 << 63) <= c[i] < 1 << 63
+        lo = c[i] & 0xFFFFFFFF
+        if i < NL - 1 and (wide >> i) & 1:
+            m = ~lo & 0xFFFFFFFF
+            c[i + 1] += 8 * s32(c[i] >> 32)
+        else:
+            m = ~lo & MASK
+            c[i + 1] += c[i] >> LB
+        for j in range(1, NL):
+            c[i + j] += m * P29[j]
+    r = [0] * NL
+    for k in range(NL, 2 * NL - 1):
+        assert -(1 << 63) <= c[k] < 1 << 63
+        c[k + 1] += c[k] >> LB
+        r[k - NL] = c[k] & MASK
+    assert 0 <= c[2 * NL - 1] < 1 << 32
+    r[NL - 1] = c[2 * NL - 1]
+    return [x & 0xFFFFFFFF for x in r]
+
+
+def test_sd_offsets_match_header():
+    src = open(os.path.join(_CSRC, "fp29.cuh")).read()
+    m = re.search(r"SD_OFF58\[2 \* NL\] = \{([^}]*)\}", src)
+    assert [int(x) for x in m.group(1).split(",")] == SD_OFF58
+    assert int(re.search(r"DELTA_SD_LOG = (\d+);", src).group(1)) == DELTA_SD_LOG
+
+
+def test_fe_mul_sd_exact_model():
+    """fe_mul_sd is a b R^-1 mod p with a normalised result < 2p, for signed differences of fe_mul
+    outputs against the unsigned forms pt_madd feeds it, random and at the interval corners."""
+    import random
+    rnd = random.Random(17)
+    Rinv = pow(R, -1, P)
+
+    def limbs(v):
+        return [(v >> (LB * i)) & MASK for i in range(NL - 1)] + [v >> (LB * (NL - 1))]
+
+    def diff(x, y):  # fe_sub_s on limbs (two's complement words)
+        return [(p - q) & 0xFFFFFFFF for p, q in zip(limbs(x), limbs(y))]
+
+    def sval(l):
+        return sum((x - (1 << 32) if x >> 31 else x) << (LB * i) for i, x in enumerate(l))
+
+    top = [MASK] * (NL - 1)
+    cases = []
+    for _ in range(2000):
+        x, y, z, w = (rnd.randrange(2 * P) for _ in range(4))
+        u = rnd.randrange(10 * P)
+        cases.append((diff(x, y), limbs(u)))                      # A = (Y - X) ymx
+        cases.append((diff(x, y), diff(z, w)))                    # X3 = E F
+        cases.append((diff(x, y), limbs(z + w)))                  # T3 = E H, Z3 = F G (sums of two)
+    # limb extremes: 0 - max and max - 0 in every limb, against maximal unsigned operands
+    mx = top + [(2 * P - 1) >> (LB * (NL - 1))]
+    neg = [(-x) & 0xFFFFFFFF for x in mx]
+    s_max = [2 * x for x in mx]
+    for a in (mx, neg):
+        for b in (mx, neg, s_max):
+            cases.append((a, b))
+    for a, b in cases:
+        r = fe_mul_sd_exact(a, b)
+        v = value_of(r)
+        assert v % P == sval(a) * sval(b) * Rinv % P
+        assert 0 <= v < 2 * P and all(x <= MASK for x in r[:NL - 1])
 
 
 def test_halved_record_is_the_same_point():
@@ -377,7 +534,13 @@ REVIEWED = {
     ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
     ("fp29.cuh", "K5P29"): "f3dc542f8a39d740",
     ("fp29.cuh", "fe_sub_v"): "b95cf1f871e652b6",
-    ("ec.cuh", "pt_madd"): "9b3453a645881673",
+    ("fp29.cuh", "fe_sub_s"): "2394a6c588a7e363",
+    ("fp29.cuh", "smad64"): "f570120e573dc55c",
+    ("fp29.cuh", "SD_OFF58"): "c88a1438ac9f5b80",
+    ("fp29.cuh", "fe_mul_sd_seed"): "d2395c468f273ed7",
+    ("fp29.cuh", "opaque_v"): "9936fb9d6abd51ca",
+    ("fp29.cuh", "fe_mul_sd"): "1524d4c9c2554e87",
+    ("ec.cuh", "pt_madd"): "940afc2112f7fd6f",
     ("ec.cuh", "pt_add"): "1449f0a88822c610",
     ("ec.cuh", "pt_dbl"): "784353f9934ef437",
     ("ec.cuh", "kt_neg_if"): "19c79f3cf45dee09",

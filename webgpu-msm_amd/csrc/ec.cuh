@@ -35,20 +35,20 @@ __device__ __forceinline__ xyzt pt_identity() {
 // acc + q (q a halved precomputed affine point, below).  add-2008-hwcd-3 with Z2 = 1, k = 2d.
 // The record holds ((y-x)/2, (y+x)/2, d*t): A, B and C come out halved, so D = 2 Z1 / 2 = Z1 needs
 // no doubling, and (X3:Y3:T3:Z3) is the sum with every coordinate scaled by 1/4 -- the same
-// projective point.  Differences carry 5p (V form) and stay unnormalised.  All outputs normalised.
+// projective point.  Differences are signed (fe_sub_s) and meet fe_mul_sd; all outputs normalised.
 __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
-  fe A = fe_mul(fe_sub_v(p.Y, p.X), q.ymx);  // V*N
-  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);    // S*N
-  fe C = fe_mul(p.T, q.kt);                  // N*N (or N*V for a negated q, kt_neg_if)
-  fe E = fe_sub_v(B, A);                     // V
-  fe F = fe_sub_v(p.Z, C);                   // V
-  fe G = fe_add(p.Z, C);                     // S
-  fe H = fe_add(B, A);                       // S
+  fe A = fe_mul_sd<WIDE_ALL, false>(fe_sub_s(p.Y, p.X), q.ymx);  // signed x N
+  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);                         // S x N
+  fe C = fe_mul(p.T, q.kt);  // N x N (or N x V for a negated q, kt_neg_if)
+  fe E = fe_sub_s(B, A);     // signed
+  fe F = fe_sub_s(p.Z, C);   // signed
+  fe G = fe_add(p.Z, C);     // S
+  fe H = fe_add(B, A);       // S
   xyzt r;
-  r.X = fe_mul_w<WIDE_EF>(E, F);  // V x V: one 29-bit reduction digit more (fp29.cuh)
-  r.Y = fe_mul(G, H);             // S x S
-  r.T = fe_mul(E, H);             // V x S
-  r.Z = fe_mul(F, G);             // V x S
+  r.X = fe_mul_sd<WIDE_ALL, true>(E, F);   // signed x signed
+  r.Y = fe_mul(G, H);                      // S x S
+  r.T = fe_mul_sd<WIDE_ALL, false>(E, H);  // signed x S
+  r.Z = fe_mul_sd<WIDE_ALL, false>(F, G);  // signed x S
   return r;
 }
 

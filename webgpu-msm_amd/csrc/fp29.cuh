@@ -180,6 +180,101 @@ __device__ __forceinline__ fe fe_mul_w(const fe& a, const fe& b) {
   return r;
 }
 
+// ---- signed differences (pt_madd) -------------------------------------------------------------
+// pt_madd's differences are plain limb-wise subtractions with no redundant multiple of p: their
+// limbs are two's-complement integers (|limb| < 2^29 for normalised operands, the top limb
+// signed), legal only as fe_mul_sd operands.  That saves the 5p offset's nine additions per
+// difference.  fe_mul_sd multiplies them with signed 32 x 32 -> 64 products (v_mad_i64_i32, the
+// same issue rate as the unsigned ones), takes its carries as arithmetic shifts, and keeps its
+// result non-negative by a bias: DELTA_SD p 2^232 joins the product through the seeds of columns
+// 8..16 (free: they start multiply-add chains), raising the result by DELTA_SD p / 2^29 = p / 8,
+// more than the most negative |a b| / 2^261 of its call sites.  The result is then an ordinary
+// fe_mul output (normalised, value in [0, 2p)).  tests/test_limb_bounds.py (fe_mul_sd) proves every
+// column register within int64 and the result range, per call site.
+__device__ __forceinline__ fe fe_sub_s(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] - b.v[i];
+  return r;
+}
+
+constexpr uint32_t DELTA_SD_LOG = 26;  // DELTA_SD = 2^26
+
+__device__ __forceinline__ uint64_t smad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)((int64_t)(int32_t)a * (int64_t)(int32_t)b) + c;
+}
+
+// With signed products a column's true range is lopsided (the reduction terms are non-negative
+// and reach ~1.3 * 2^63 in the middle columns), so every column register also carries an offset
+// O_k = SD_OFF58[k] * 2^58 that centres its range in int64.  O_k is a multiple of 2^32, so the
+// low word (the reduction digit) is untouched and the carry out grows by exactly O_k / 2^29,
+// which the next column's seed takes back.
+__device__ constexpr int8_t SD_OFF58[2 * NL] = {-1, -3, -3, -5, -9, -9, -12, -14, -14, -12, -11, -9, -6, -5, -2, -1, -1, 0};
+
+__device__ constexpr uint64_t fe_mul_sd_seed(uint32_t wide, int k, uint32_t p_k8) {
+  // fe_mul_seed's register offset, the bias DELTA_SD p_(k-8) on columns 8..16, and the centring
+  // offset O_k less the previous column's O_(k-1) / 2^29 (its carry's excess)
+  return (k <= NL ? fe_mul_seed(wide, k) : 0ull) + ((k >= NL - 1 && k < 2 * NL - 1) ? (uint64_t)p_k8 << DELTA_SD_LOG : 0ull) +
+         (uint64_t)((int64_t)SD_OFF58[k] * (1ll << 58)) -
+         (k >= 1 ? (uint64_t)((int64_t)SD_OFF58[k - 1] * (1ll << 29)) : 0ull);
+}
+
+// a b 2^-261 mod p with a signed (fe_sub_s) and b signed too (SB) or an unsigned form < 2^31.
+__device__ __forceinline__ uint32_t opaque_v(uint32_t v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
+template <uint32_t WIDE, bool SB>
+__device__ __forceinline__ fe fe_mul_sd(const fe& a_in, const fe& b_in) {
+  // Operands through an empty asm: LLVM otherwise proves some limbs non-negative (masked) and
+  // lowers their sign-extended products as unsigned products plus sign corrections.
+  fe a, b;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    a.v[i] = opaque_v(a_in.v[i]);
+    b.v[i] = opaque_v(b_in.v[i]);
+  }
+  uint64_t c[2 * NL];
+  const uint32_t eight = opaque_s(8u);
+#define MSM_SD_SEED(k) fe_mul_sd_seed(WIDE, (k), (k) >= NL - 1 && (k) < 2 * NL - 1 ? P29[(k) - (NL - 1)] : 0u)
+#pragma unroll
+  for (int k = 0; k < NL; k++) c[k] = seeded(smad64(a.v[0], b.v[k], MSM_SD_SEED(k)));
+  c[NL] = seeded(smad64(a.v[1], b.v[NL - 1], MSM_SD_SEED(NL)));
+#pragma unroll
+  for (int k = NL + 1; k < 2 * NL; k++) c[k] = MSM_SD_SEED(k);
+#undef MSM_SD_SEED
+#pragma unroll
+  for (int i = 1; i < NL; i++)
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+      if (i == 1 && j == NL - 1) continue;  // issued above as a seeded product
+      c[i + j] = seeded(smad64(a.v[i], b.v[j], c[i + j]));
+    }
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t lo = (uint32_t)c[i];
+    uint32_t m;
+    if (i < NL - 1 && ((WIDE >> i) & 1u)) {
+      m = ~lo;
+      c[i + 1] = seeded(smad64((uint32_t)(c[i] >> 32), eight, c[i + 1]));  // 8 * (signed high word)
+    } else {
+      m = ~lo & LMASK;
+      c[i + 1] += (uint64_t)((int64_t)c[i] >> LBITS);
+    }
+#pragma unroll
+    for (int j = 1; j < NL; j++) c[i + j] = mad64(m, P29[j], c[i + j]);
+  }
+  fe r;
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    c[k + 1] += (uint64_t)((int64_t)c[k] >> LBITS);
+    r.v[k - NL] = (uint32_t)c[k] & LMASK;
+  }
+  r.v[NL - 1] = (uint32_t)c[2 * NL - 1];
+  return r;
+}
+
 // Every operand pair but the S x (1.5 | U) products named above: all eight low digits wide.
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) { return fe_mul_w<WIDE_ALL>(a, b); }
 
