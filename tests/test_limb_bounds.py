@@ -9,7 +9,9 @@ arithmetic on the limb maxima) and asserts:
   * every fe_mul column stays < 2^64 (products + reduction terms + incoming carry);
   * every fe_mul operand pair keeps a*b < p * 2^261, so the lazy result is < 2p (no final
     subtraction needed);
-  * fe_sub / fe_neg never produce a negative limb (K8P dominates the subtrahend limb-wise).
+  * fe_sub / fe_neg never produce a negative limb (K8P dominates the subtrahend limb-wise);
+  * pt_madd's signed differences (fe_sub_s) keep every fe_mul_sd column register inside int64
+    (per-limb intervals, with the centring offsets SD_OFF58) and its biased result in [0, 2p).
 
 It mirrors the kernels by hand; test_mirrored_sources_unchanged pins a digest of every mirrored
 function body, so an edit to fp29.cuh / ec.cuh fails until the model here is re-reviewed.
