@@ -53,11 +53,12 @@ __host__ __device__ inline uint32_t win_off(const MsmDims& d, uint32_t w) {
 
 constexpr uint32_t PT_WORDS = 36;  // extended point, 4 x 9 limbs (144 B)
 // Precomputed affine point record, 128 B (one cache line), in two 48-B halves the gather can swap:
-//   words  0..8  (y-x)/2   9 d*t limb 8   10..11 zero
-//   words 12..20 (y+x)/2  21 d*t limb 8   22..23 zero
+//   words  0..8  (y-x)/2   9 d*t limb 8   10 (y+x)/2 limb 8   11 zero
+//   words 12..20 (y+x)/2  21 d*t limb 8   22 (y-x)/2 limb 8   23 zero
 //   words 24..31 d*t limbs 0..7
 // A negated point (-x, y) swaps (y-x)/2 and (y+x)/2: k_accumulate reads the half at PRE_HALF * sign
-// first, so the swap is an address offset, not 18 selects (load_pre_signed).
+// first, so the swap is an address offset, not 18 selects (load_pre_signed).  The half read first
+// (12 words) holds every top limb, so the other half costs only its 8 low words: 7 loads.
 constexpr uint32_t PRE_WORDS = 32;
 constexpr uint32_t PRE_HALF = 12;  // words per swappable half
 constexpr uint32_t PRE_KT = 24;    // d*t limbs 0..7

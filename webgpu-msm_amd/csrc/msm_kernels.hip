@@ -142,7 +142,11 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
   }
 #pragma unroll
   for (int k = 0; k < NL - 1; k++) rec[PRE_KT + k] = kt.v[k];
-  rec[NL] = rec[PRE_HALF + NL] = kt.v[NL - 1];  // in both halves: read from whichever comes first
+  // each half also carries d*t's top limb and the OTHER half's top limb: the half read first
+  // supplies both, so the half read second needs only its eight low limbs (seven loads in all)
+  rec[NL] = rec[PRE_HALF + NL] = kt.v[NL - 1];
+  rec[NL + 1] = ypx.v[NL - 1];
+  rec[PRE_HALF + NL + 1] = ymx.v[NL - 1];
 #pragma unroll
   for (uint32_t q = 0; q < 8; q++)
     st[pp_slot(i, q)] = make_uint4(rec[4 * q], rec[4 * q + 1], rec[4 * q + 2], rec[4 * q + 3]);
@@ -189,9 +193,9 @@ __device__ __forceinline__ pre load_pre_signed(const uint32_t* __restrict__ pts,
   const uint32_t* h0 = reinterpret_cast<const uint32_t*>(rec + o0);
   const uint32_t* h1 = reinterpret_cast<const uint32_t*>(rec + (o0 ^ (PRE_HALF * 4)));
   const uint4 a0 = reinterpret_cast<const uint4*>(h0)[0], a1 = reinterpret_cast<const uint4*>(h0)[1];
-  const uint2 a2 = reinterpret_cast<const uint2*>(h0)[4];
+  const uint4 a2 = reinterpret_cast<const uint4*>(h0)[2];  // top limb, d*t's top limb, the other half's top limb
   const uint4 b0 = reinterpret_cast<const uint4*>(h1)[0], b1 = reinterpret_cast<const uint4*>(h1)[1];
-  const uint32_t b2 = h1[8];
+  const uint32_t b2 = a2.z;
   const uint4 c0 = reinterpret_cast<const uint4*>(rec + PRE_KT * 4)[0];
   const uint4 c1 = reinterpret_cast<const uint4*>(rec + PRE_KT * 4)[1];
   const uint32_t av[NL] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x};
