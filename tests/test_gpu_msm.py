@@ -49,6 +49,25 @@ def test_field_ops_random():
         assert _from_le(k2d[i]) == 6042 * a[i] % O.P
 
 
+def test_signed_difference_multiply():
+    """fe_mul_sd (pt_madd's products of signed differences) on the device: (a - b)(b - a) and
+    (a - b)(a + b) mod p for random operands and the edge values, bit-exact against Python."""
+    rng = np.random.default_rng(23)
+    a = [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(4096)]
+    b = [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(4096)]
+    edge = [0, 1, 2, O.P - 1, O.P - 2, (O.P - 1) // 2, 1 << 252]
+    for x in edge:
+        for y in edge:
+            a.append(x)
+            b.append(y)
+    A, B = _le_words(a), _le_words(b)
+    neg_sq = M._test_field_op(4, A, B)
+    diff_sq = M._test_field_op(5, A, B)
+    for i in range(len(a)):
+        assert _from_le(neg_sq[i]) == -(a[i] - b[i]) ** 2 % O.P, i
+        assert _from_le(diff_sq[i]) == (a[i] * a[i] - b[i] * b[i]) % O.P, i
+
+
 def test_point_ops_vs_oracle(golden):
     rng = np.random.default_rng(3)
     ks = [int(rng.integers(1, 2**62)) for _ in range(64)]

@@ -1319,7 +1319,13 @@ extern "C" __global__ void k_test_field(const uint32_t* __restrict__ a, const ui
     bw[k] = b[(size_t)i * 8 + k];
   }
   fe x = fe_to_mont(fe_from_words_le(aw)), y = fe_to_mont(fe_from_words_le(bw));
-  fe r = op == 0 ? fe_mul(x, y) : op == 1 ? fe_add_n(x, y) : op == 2 ? fe_sub(x, y) : fe_mul_2d(x);
+  // ops 4, 5: pt_madd's signed-difference multiply, (x - y)(y - x) and (x - y)(x + y)
+  fe r = op == 0   ? fe_mul(x, y)
+         : op == 1 ? fe_add_n(x, y)
+         : op == 2 ? fe_sub(x, y)
+         : op == 3 ? fe_mul_2d(x)
+         : op == 4 ? fe_mul_sd<WIDE_ALL, true>(fe_sub_s(x, y), fe_sub_s(y, x))
+                   : fe_mul_sd<WIDE_ALL, false>(fe_sub_s(x, y), fe_add(x, y));
   fe_to_words_le(fe_to_std(r), ow);
 #pragma unroll
   for (int k = 0; k < 8; k++) out[(size_t)i * 8 + k] = ow[k];
