@@ -227,3 +227,22 @@ def test_host_inverse_matches_fermat():
     bad = ctypes.c_double(-1)
     assert L.msm_test_host_timing(4, 4000, ctypes.byref(bad)) == 0
     assert bad.value == 0
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N without torchrun measures N devices in one process; with fewer gfx950
+    devices visible (none in the CPU container) it exits non-zero and prints no JSON line."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    import msm_amd as M
+
+    n = len(M.device_ordinals())
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(max(n + 1, 2)), "--steps", "1",
+                        "--no-extras", "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert "gfx950 device(s) visible" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

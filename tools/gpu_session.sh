@@ -24,6 +24,10 @@
 #                launches kernel_ms measures)
 #   kstats1lib:LIBS  kstats1 for each in-tree library variant (names suffixed with $KS if set)
 #   latprof      rocprofv3 kernel trace of single-MSM latency runs (tools/timeline.py reads it)
+#   e2etrace     rocprofv3 kernel + memory-copy trace of msm_compute from host arrays (tools/e2e_probe.py)
+#   e2e          msm_compute from host arrays, wall times only
+#   e2esrc       the same with the inputs in numpy / no-huge-page / MAP_SHARED host memory
+#   h2d          the host->device upload microbenchmark (tools/ubench/h2d_bench)
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3); $BENCH_X adds bench.py
@@ -123,6 +127,13 @@ for step in "$@"; do
     latprof)
       run latprof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_latprof_d -o run \
         -- python3 tools/latency_probe.py --runs 12 ;;
+    e2etrace)  # kernels + host->device copies of msm_compute from host arrays (2^20)
+      run e2etrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+        -d gpurun_out/${TAG}_e2etrace_d -o run -- python3 tools/e2e_probe.py --runs 8 ;;
+    e2e) run e2e 120 python tools/e2e_probe.py --runs 12 ;;
+    e2esrc)  # msm_compute from host arrays in numpy / no-huge-page / MAP_SHARED memory
+      for src in numpy nohuge shared; do run "e2e_$src" 120 python tools/e2e_probe.py --runs 10 --src "$src"; done ;;
+    h2d) run h2d 120 tools/ubench/h2d_bench ;;
     pmc) run pmc 900 bash tools/profile_pmc.sh "$TAG" ;;
     ab:*)
       IFS=: read -r _ libs rounds <<< "$step"

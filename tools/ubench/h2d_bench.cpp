@@ -2,6 +2,7 @@
 // msm_compute.  Prints one JSON line per measurement.
 //   hipcc -O2 -std=c++17 --offload-arch=gfx950 -o h2d_bench h2d_bench.cpp -lpthread
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -104,6 +105,31 @@ int main(int argc, char** argv) {
     CK(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, s));
     CK(hipStreamSynchronize(s));
     if (r == 2) rep("pageable_memcpy", ms_since(t0));
+  }
+  // pageable sources by page type: the copy engine's rate depends on how the source is mapped
+  // (numpy's large arrays are transparent-huge-page backed; a Node SharedArrayBuffer need not be)
+  for (int kind = 0; kind < 4; kind++) {
+    static const char* names[4] = {"src_thp_madvise", "src_nohugepage", "src_mmap_shared", "src_mmap_private"};
+    char* src = nullptr;
+    if (kind < 2) {
+      src = (char*)aligned_alloc(2 * MB, total);
+      madvise(src, total, kind == 0 ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+    } else {
+      void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, (kind == 2 ? MAP_SHARED : MAP_PRIVATE) | MAP_ANONYMOUS, -1, 0);
+      if (m == MAP_FAILED) continue;
+      src = (char*)m;
+    }
+    memcpy(src, host, total);
+    double best = 1e9;
+    for (int r = 0; r < 4; r++) {
+      auto t0 = clk::now();
+      CK(hipMemcpyAsync(dev, src, total, hipMemcpyHostToDevice, s));
+      CK(hipStreamSynchronize(s));
+      if (r) best = std::min(best, ms_since(t0));
+    }
+    rep(names[kind], best);
+    if (kind < 2) free(src);
+    else munmap(src, total);
   }
   // pinned source
   char* pin;

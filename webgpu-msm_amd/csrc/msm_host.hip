@@ -1676,8 +1676,35 @@ int multi_host_entry(const uint32_t* points_be, const uint32_t* scalars_be, size
   return sharded_host(points_be, scalars_be, n, opts, devs, r);
 }
 
+// Peer access of the current device `dev` to `owner`'s memory, enabled once per ordered pair, so
+// the peer copies of peer_shard run device to device over xGMI (without it the runtime may stage
+// them through host memory).  "Already enabled" (another library in the process, e.g. RCCL, did it)
+// counts as enabled; a pair without peer support is remembered and left to the runtime's staged
+// copies.  Returns 1 when enabled, 0 otherwise (msm_test_peer_state).
+std::mutex g_peer_mu;
+std::vector<int8_t> g_peer;  // [g_nhip * g_nhip]: 0 untried, 1 enabled, -1 unavailable
+
+int enable_peer(int dev, int owner) {
+  if (dev == owner) return 1;
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  if (g_nhip <= 0 || dev >= g_nhip || owner >= g_nhip) return 0;
+  if (g_peer.size() != (size_t)g_nhip * g_nhip) g_peer.assign((size_t)g_nhip * g_nhip, 0);
+  int8_t& st = g_peer[(size_t)dev * g_nhip + owner];
+  if (st == 0) {
+    int can = 0;
+    st = -1;
+    if (hipDeviceCanAccessPeer(&can, dev, owner) == hipSuccess && can) {
+      const hipError_t e = hipDeviceEnablePeerAccess(owner, 0);
+      if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) st = 1;
+    }
+    (void)hipGetLastError();  // a refused enable leaves no sticky error for the next call
+  }
+  return st > 0 ? 1 : 0;
+}
+
 // One shard of device-resident inputs that live on another device: copied over xGMI (a peer copy
-// on the slot's stream) into this device's wire buffers, then reduced here.
+// on the slot's stream, peer access enabled first) into this device's wire buffers, then reduced
+// here.
 int peer_shard(int owner, const uint32_t* d_points, const uint32_t* d_scalars, size_t cnt, const msm_opts* od,
                Pt* r) {
   return on_device(od, [&](DevCtx* c) -> int {
@@ -1685,6 +1712,7 @@ int peer_shard(int owner, const uint32_t* d_points, const uint32_t* d_scalars, s
       *r = msmh::pt_identity();
       return MSM_OK;
     }
+    enable_peer(c->device, owner);
     Slot& sl = c->slot[0];
     Workspace& w = sl.ws;
     int rc;
@@ -2097,6 +2125,15 @@ int msm_test_sharded(int mode, const uint32_t* points, const uint32_t* scalars, 
   if (rc != MSM_OK) return rc;
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
+}
+
+// Peer access of device `dev` to `owner` (enabled on first use, as peer_shard does): 1 enabled
+// (or dev == owner), 0 unavailable, MSM_ERR_INVALID_ARG for a non-gfx950 ordinal.
+int msm_test_peer_state(int dev, int owner) {
+  DevCtx *a, *b;
+  if (get_ctx(dev, &a) != MSM_OK || get_ctx(owner, &b) != MSM_OK) return MSM_ERR_INVALID_ARG;
+  DeviceGuard g(dev);
+  return enable_peer(dev, owner);
 }
 
 // The host tail of a lone MSM of n points (auto plan) on caller-supplied window terms (host

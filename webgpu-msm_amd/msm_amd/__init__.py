@@ -127,6 +127,7 @@ def load() -> ctypes.CDLL:
                               u32p], ctypes.c_int),
         "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_tail_words": ([sz], sz),
+        "msm_test_peer_state": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -432,7 +433,7 @@ def compute_msm_cpu(points_wire, scalars_wire, window_size: Optional[int] = None
 
 def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_size: Optional[int] = None,
                                     run_length: Optional[int] = None, device: int = -1,
-                                    stream: int = 0) -> np.ndarray:
+                                    stream: int = 0, flags: int = 0) -> np.ndarray:
     """compute_msm_many_device, each result as a projective X|Y|T|Z partial: [count][32] BE words."""
     L = load()
     count = len(points_list)
@@ -442,7 +443,7 @@ def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_si
     ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
     o, op = _out(32 * max(count, 1))
     _check(L.msm_compute_many_device_partial(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n,
-                                             count, _opts(window_size, run_length, device),
+                                             count, _opts(window_size, run_length, device, flags),
                                              _stream(stream, _first(points_list), _first(scalars_list)), op),
            "msm_compute_many_device_partial")
     return o[:32 * count].reshape(count, 32)
