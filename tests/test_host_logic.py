@@ -211,12 +211,14 @@ def test_lone_msm_tail_threads_agree(n):
         for j, v in enumerate((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)):
             terms[i * 32 + 8 * j: i * 32 + 8 * j + 8] = _host_mont_words(v)
     got = {}
-    for helpers in (0, 1, 3):
+    # helpers < 0: one persistent crew over 40 rounds, some armed and disarmed without terms (the
+    # per-device crew of lone MSMs, including their error returns)
+    for helpers in (0, 1, 3, -3, -1):
         out = (ctypes.c_uint32 * 16)()
         ms = ctypes.c_double()
-        assert L.msm_test_tail(n, terms.ctypes.data, helpers, out, ctypes.byref(ms)) == 0
+        assert L.msm_test_tail(n, terms.ctypes.data, helpers, out, ctypes.byref(ms)) == 0, helpers
         got[helpers] = (M.wire_to_int(out[:8]), M.wire_to_int(out[8:]))
-    assert got[0] == got[1] == got[3]
+    assert got[0] == got[1] == got[3] == got[-3] == got[-1]
 
 
 def test_host_inverse_matches_fermat():

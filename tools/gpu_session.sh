@@ -28,6 +28,10 @@
 #   e2e          msm_compute from host arrays, wall times only
 #   e2esrc       the same with the inputs in numpy / no-huge-page / MAP_SHARED host memory
 #   h2d          the host->device upload microbenchmark (tools/ubench/h2d_bench)
+#   e2erocm      msm_compute from host arrays on /opt/rocm's HIP runtime (no torch loaded)
+#   e2eenv:VAR=A,B[:R]  msm_compute from host arrays over values of one knob (interleaved)
+#   node         the Node flat-buffer compute_msm (tools/node_flat.mjs), shared and plain buffers
+#   nodetrace    rocprofv3 kernel + memory-copy trace of the Node shared-buffer path
 #   pmc          the PMC passes of tools/profile_pmc.sh (one counter group per rocprofv3 run)
 #   ab:LIBS[:R]  interleaved bench A/B of in-tree library variants (comma-separated file names
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3); $BENCH_X adds bench.py
@@ -134,6 +138,26 @@ for step in "$@"; do
     e2esrc)  # msm_compute from host arrays in numpy / no-huge-page / MAP_SHARED memory
       for src in numpy nohuge shared; do run "e2e_$src" 120 python tools/e2e_probe.py --runs 10 --src "$src"; done ;;
     h2d) run h2d 120 tools/ubench/h2d_bench ;;
+    e2eenv:*)  # e2eenv:VAR=A,B[:R] -- msm_compute from host arrays over values of one knob, interleaved
+      IFS=: read -r _ spec rounds <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for r in $(seq 1 "${rounds:-2}"); do
+        for v in ${vals//,/ }; do
+          export "$var=$v"
+          run "e2eenv_${var}_${v}_$r" 120 python tools/e2e_probe.py --runs 12
+          unset "$var"
+        done
+      done ;;
+    e2erocm)  # msm_compute on /opt/rocm's HIP runtime (no torch in the process), as Node and C callers run
+      MSM_AMD_NO_TORCH=1 run e2e_rocm 120 python tools/e2e_probe.py --runs 10 ;;
+    node)  # the Node flat-buffer compute_msm (SharedArrayBuffer, then plain ArrayBuffer)
+      run node_inputs 120 python tools/write_inputs.py /tmp/msm_in
+      run node_shared 120 node tools/node_flat.mjs /tmp/msm_in/p.bin /tmp/msm_in/s.bin 1048576 8 shared
+      run node_plain 120 node tools/node_flat.mjs /tmp/msm_in/p.bin /tmp/msm_in/s.bin 1048576 8 plain ;;
+    nodetrace)
+      run node_inputs 120 python tools/write_inputs.py /tmp/msm_in
+      run nodetrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/${TAG}_nodetrace_d \
+        -o run -- node tools/node_flat.mjs /tmp/msm_in/p.bin /tmp/msm_in/s.bin 1048576 6 shared ;;
     pmc) run pmc 900 bash tools/profile_pmc.sh "$TAG" ;;
     ab:*)
       IFS=: read -r _ libs rounds <<< "$step"

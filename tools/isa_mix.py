@@ -16,6 +16,14 @@ the hash and reports no floor on a mismatch).  The basic block of k_accumulate h
     per second over all 256 CUs), so clock and encoding effects are in the price.
 bench.py turns these into the ISA floor of the kernel: floor = (entries / 64) x ns_per_iteration_chip,
 frac_isa_measured = floor / k_accumulate duration.
+
+The loop's other blocks are priced too (`loop_classes`), by what runs them: the blocks every
+wave-iteration passes (loop header, exec-mask joins, the entry select), the sorted-entry vector
+load (every fourth iteration), and the bucket-boundary path -- the finished bucket's store, the
+accumulator reset and the advance to the next bucket (a wave runs it whenever ANY of its 64 lanes
+reaches a bucket end) and the run head's LDS staging (a lane's first bucket end).  bench.py weights
+them by their execution frequency for the launch's entries and buckets and adds
+them to the floor.
 """
 import argparse
 import collections
@@ -41,23 +49,74 @@ def asm_text(tmp):
 
 
 def blocks_of(asm, func):
+    """{block: [opcodes]} of `func`, and the blocks of its loops (the assembler's "in Loop" /
+    "Loop Header" annotations on the label line or the comment lines right after it)."""
+    blocks, depth = basic_blocks(asm, func)
+    return blocks, {b for b, d in depth.items() if d >= 1}
+
+
+def basic_blocks(asm, func):
+    """Basic blocks split at every label (.LBB) and fall-through block comment (; %bb.N:), with
+    each block's loop depth (0 outside loops)."""
     lines = asm.splitlines()
     start = next(i for i, l in enumerate(lines) if l.startswith(func + ":"))
-    out, loops, cur = {}, set(), None
+    out, depth, cur, head = {}, {}, None, False
     for l in lines[start:]:
         if l.startswith(".Lfunc_end"):
             break
-        m = re.match(r"^(\.LBB\w+|" + func + r"):", l)
+        m = re.match(r"^(\.LBB\w+|" + func + r"):", l) or re.match(r"^; (%bb\.\d+):", l)
         if m:
             cur = m.group(1)
-            out[cur] = []
-            if "Loop" in l:  # the assembler's "in Loop: Header=..." / "Loop Header" annotation
-                loops.add(cur)
-            continue
+            out[cur], depth[cur], head = [], 0, True
         s = l.strip()
-        if cur and s and not s.startswith((";", ".")):
+        if head and ";" in l:  # the label line's annotation, then comment-only lines after it
+            d = re.search(r"Depth=(\d+)", l)
+            if d:
+                depth[cur] = max(depth[cur], int(d.group(1)))
+            elif "Loop" in l:
+                depth[cur] = max(depth[cur], 1)
+            if not m and not s.startswith(";"):
+                head = False
+        elif not m:
+            head = False
+        if cur and s and not s.startswith((";", ".")) and not m:
             out[cur].append(s.split()[0])
-    return out, loops
+            if s.startswith("s_cbranch") or s.startswith("s_branch"):
+                TARGETS.setdefault(cur, set()).add(s.split()[-1])
+    return out, depth
+
+
+TARGETS = {}  # block -> labels it branches to (filled by basic_blocks)
+
+
+def classify_loop(blocks, depth, main, targets=None):
+    """Classes of the depth-1 loop blocks other than the main (mixed-add) block, by what they hold:
+    'boundary' (bucket-end store, accumulator reset: >= 18 moves, advance), 'head' (LDS staging of a
+    run's head), 'vecload' (the every-fourth-iteration entry load), 'gallop' (the inner search
+    loops over empty buckets, depth 2), 'iteration' (everything else: every wave-iteration)."""
+    targets = targets or {}
+    cls = {}
+    for b, ops in blocks.items():
+        if b == main or depth.get(b, 0) < 1:
+            continue
+        if depth[b] >= 2:
+            cls[b] = "gallop"
+        elif any(o.startswith("ds_write") for o in ops):
+            cls[b] = "head"
+        elif any(o.startswith("global_store") for o in ops):
+            cls[b] = "boundary"
+        elif sum(1 for o in ops if o.startswith("v_mov_b32")) >= 18:
+            cls[b] = "boundary"  # the accumulator reset to the identity
+        elif any(o.startswith("global_load_dwordx4") for o in ops):
+            cls[b] = "vecload"
+        elif any(o == "global_load_dword" for o in ops):
+            # one-word loads outside the mixed add: the per-entry load of runs that are not 16-B
+            # aligned (it branches straight back into the main block; unused when K % 4 == 0), or
+            # the search over empty buckets (rare with random scalars)
+            cls[b] = "scalar_entry" if main in targets.get(b, ()) else "gallop"
+        else:
+            cls[b] = "iteration"
+    return cls
 
 
 # instructions the rate benchmark does not time, priced as the measured instruction of their
@@ -105,10 +164,12 @@ def main():
     args = ap.parse_args()
     if args.asm:
         with open(args.asm) as f:
-            blocks, loops = blocks_of(f.read(), args.func)
+            asm = f.read()
     else:
         with tempfile.TemporaryDirectory() as tmp:
-            blocks, loops = blocks_of(asm_text(tmp), args.func)
+            asm = asm_text(tmp)
+    blocks, loops = blocks_of(asm, args.func)
+    _, depth = basic_blocks(asm, args.func)
     # the loop block with the most multiplies: one entry's pt_madd per wave-iteration
     name, ins = max(((k, v) for k, v in blocks.items() if k in loops),
                     key=lambda kv: sum(1 for o in kv[1] if o in MADS))
@@ -141,6 +202,23 @@ def main():
         with open(args.lib, "rb") as f:
             res["lib_sha256"] = hashlib.sha256(f.read()).hexdigest()
         res["lib"] = os.path.basename(args.lib)
+    # the loop's other blocks, by class (priced below when the rates file is present)
+    cls = classify_loop(blocks, depth, name, TARGETS)
+    classes = {}
+    for b, k in cls.items():
+        if b in merged:
+            continue
+        c = classes.setdefault(k, {"blocks": [], "instructions": 0, "valu": 0, "mix": collections.Counter()})
+        c["blocks"].append(b)
+        c["instructions"] += len(blocks[b])
+        c["valu"] += sum(1 for o in blocks[b] if o.startswith("v_"))
+        c["mix"].update(base(o) for o in blocks[b])
+    if os.path.exists(args.rates):
+        for k, c in classes.items():
+            c["ns_chip"], _ = price_measured(c["mix"], args.rates)
+    for c in classes.values():
+        c["mix"] = dict(c["mix"].most_common())
+    res["loop_classes"] = classes
     if os.path.exists(args.rates):
         ns, unpriced = price_measured(cnt, args.rates)
         res["ns_per_iteration_chip"] = ns

@@ -1,76 +1,89 @@
 // End-to-end compute_msm time through the Node surface, the reference's own timing semantics
-// (src/ui/Benchmark.tsx:29-39: performance.now() around `await msmFunc(points, scalars)`, with
-// the U32ArrayPoint[] / Uint32Array[] inputs AllBenchmarks.tsx:81-94 builds).
+// (src/ui/Benchmark.tsx:29-39: performance.now() around `await msmFunc(points, scalars)`), for the
+// input forms the reference's callers use:
+//   flat_input_ms        flat wire buffers over a SharedArrayBuffer (what submission.ts:35-39
+//                        allocates; read in place by the addon)
+//   flat_copied_input_ms flat wire buffers over a plain ArrayBuffer (copied by the addon first)
+//   node_e2e_ms          U32ArrayPoint[] / Uint32Array[] objects (AllBenchmarks.tsx:81-94), with
+//                        marshal_ms = their JS flatten alone (flattenU32)
+//   bigint_input_ms      BigIntPoint[] / bigint[] (the test-data loader's form, testCases.ts:34-52),
+//                        marshalled natively by the addon (napi_get_value_bigint_words)
+// The flat forms run first, on a fresh heap: millions of live point objects make V8's collector
+// pause the main thread, which delays the promise's resolution (the round-3 harness measured the
+// flat forms after building the objects and read 7-9 ms for a 4 ms call).
 //
-//   node --max-old-space-size=8192 tools/node_e2e.mjs <points.bin> <scalars.bin> <n> <runs> [x y]
+//   node --max-old-space-size=16384 tools/node_e2e.mjs <points.bin> <scalars.bin> <n> <runs> [x y]
 //
 // points.bin / scalars.bin: wire words (x|y|t|z BE u32[8] each / BE u32[8]), as bench.py writes
-// them.  Prints one JSON line: median and all run times (ms), and whether every result matched.
+// them.  Prints one JSON line: medians and all run times (ms), and whether every result matched.
 import fs from "fs";
 import { performance } from "perf_hooks";
-import { compute_msm, flattenU32 } from "../webgpu-msm_amd/js/submission.mjs";
+import { compute_msm, flattenU32, u32ArrayToBigInts } from "../webgpu-msm_amd/js/submission.mjs";
 
 const [, , pPath, sPath, nArg, runsArg, xArg, yArg] = process.argv;
 const n = parseInt(nArg, 10);
 const runs = parseInt(runsArg || "5", 10);
-const pw = new Uint32Array(fs.readFileSync(pPath).buffer.slice(0));
-const sw = new Uint32Array(fs.readFileSync(sPath).buffer.slice(0));
-// one Uint32Array per coordinate and per scalar, as bigIntToU32Array gives the harness
-const points = new Array(n);
-const scalars = new Array(n);
-for (let i = 0; i < n; i++) {
-  const o = 32 * i;
-  points[i] = {
-    x: pw.slice(o, o + 8),
-    y: pw.slice(o + 8, o + 16),
-    t: pw.slice(o + 16, o + 24),
-    z: pw.slice(o + 24, o + 32),
-  };
-  scalars[i] = sw.slice(8 * i, 8 * i + 8);
-}
 const expect = xArg ? { x: BigInt(xArg), y: BigInt(yArg) } : null;
-(async () => {
-  const times = [];
-  let ok = true;
+const med = (xs) => [...xs].sort((a, b) => a - b)[Math.floor(xs.length / 2)];
+let ok = true;
+
+// runs + 1 awaited calls of compute_msm(p(), s()); the first warms the addon, context and graphs
+async function timeCalls(p, s) {
+  const ts = [];
   for (let r = 0; r <= runs; r++) {
     const t0 = performance.now();
-    const res = await compute_msm(points, scalars);
+    const res = await compute_msm(p, s);
     const t1 = performance.now();
-    if (r > 0) times.push(t1 - t0); // run 0 warms the addon, device context and graphs
+    if (r > 0) ts.push(t1 - t0);
     if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
   }
-  // the JS marshalling share alone: compute_msm's flatten of the U32ArrayPoint[] objects
+  return ts;
+}
+
+(async () => {
+  let pw = new Uint32Array(fs.readFileSync(pPath).buffer.slice(0));
+  let sw = new Uint32Array(fs.readFileSync(sPath).buffer.slice(0));
+  const share = (a) => {
+    const b = new Uint32Array(new SharedArrayBuffer(a.length * 4));
+    b.set(a);
+    return b;
+  };
+  let spw = share(pw), ssw = share(sw);
+  const flatTimes = await timeCalls(spw, ssw);
+  const copyTimes = await timeCalls(pw, sw);
+  spw = ssw = null;
+  // U32ArrayPoint[] objects: one Uint32Array per coordinate and per scalar, as bigIntToU32Array
+  // gives the reference's harness
+  let points = new Array(n);
+  let scalars = new Array(n);
+  for (let i = 0; i < n; i++) {
+    const o = 32 * i;
+    points[i] = { x: pw.slice(o, o + 8), y: pw.slice(o + 8, o + 16), t: pw.slice(o + 16, o + 24), z: pw.slice(o + 24, o + 32) };
+    scalars[i] = sw.slice(8 * i, 8 * i + 8);
+  }
+  const objTimes = await timeCalls(points, scalars);
   const flat = [];
   for (let r = 0; r < runs; r++) {
     const t0 = performance.now();
     flattenU32(points, scalars);
     flat.push(performance.now() - t0);
   }
-  // the same MSM from flat wire buffers (no marshalling): the addon + libmsm share.  Over a
-  // SharedArrayBuffer (as the reference allocates its buffers, submission.ts:35-39) the addon reads
-  // them in place; over a plain ArrayBuffer (pw, sw) it copies them first (detachable memory).
-  const share = (a) => {
-    const b = new Uint32Array(new SharedArrayBuffer(a.length * 4));
-    b.set(a);
-    return b;
-  };
-  const spw = share(pw), ssw = share(sw);
-  const timeFlat = async (p, s) => {
-    const ts = [];
-    for (let r = 0; r <= runs; r++) {
-      const t0 = performance.now();
-      const res = await compute_msm(p, s);
-      const t1 = performance.now();
-      if (r > 0) ts.push(t1 - t0);
-      if (expect && (res.x !== expect.x || res.y !== expect.y)) ok = false;
-    }
-    return ts;
-  };
-  const flatTimes = await timeFlat(spw, ssw);
-  const copyTimes = await timeFlat(pw, sw);
-  const med = (xs) => [...xs].sort((a, b) => a - b)[Math.floor(xs.length / 2)];
-  console.log(JSON.stringify({ node_e2e_ms: med(times), marshal_ms: med(flat), flat_input_ms: med(flatTimes),
-                               flat_copied_input_ms: med(copyTimes), runs_ms: times, correct: expect ? ok : null }));
+  points = scalars = null;
+  // BigIntPoint[] / bigint[]
+  const big = (o) => u32ArrayToBigInts(pw.subarray(o, o + 8))[0];
+  let bpoints = new Array(n);
+  let bscalars = new Array(n);
+  for (let i = 0; i < n; i++) {
+    const o = 32 * i;
+    bpoints[i] = { x: big(o), y: big(o + 8), t: big(o + 16), z: big(o + 24) };
+    bscalars[i] = u32ArrayToBigInts(sw.subarray(8 * i, 8 * i + 8))[0];
+  }
+  const bigTimes = await timeCalls(bpoints, bscalars);
+  console.log(JSON.stringify({
+    flat_input_ms: med(flatTimes), flat_copied_input_ms: med(copyTimes), node_e2e_ms: med(objTimes),
+    marshal_ms: med(flat), bigint_input_ms: med(bigTimes), runs_ms: { flat: flatTimes, flat_copied: copyTimes,
+    objects: objTimes, bigint: bigTimes }, correct: expect ? ok : null,
+  }));
 })().catch((e) => {
   console.log(JSON.stringify({ error: String(e) }));
   process.exit(1);

@@ -131,6 +131,31 @@ int main(int argc, char** argv) {
     if (kind < 2) free(src);
     else munmap(src, total);
   }
+  // pageable source in pieces (the host-input split's copies): one stream, or alternating over two
+  // streams (whether a second copy queue hides the ~20 us gap between consecutive copies)
+  {
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    for (int pieces : {8, 10, 16}) {
+      for (int streams : {1, 2}) {
+        double best = 1e9;
+        for (int r = 0; r < 3; r++) {
+          const size_t per = total / pieces;
+          auto t0 = clk::now();
+          for (int k = 0; k < pieces; k++)
+            CK(hipMemcpyAsync((char*)dev + k * per, host + k * per, per, hipMemcpyHostToDevice,
+                              (streams == 2 && (k & 1)) ? s2 : s));
+          CK(hipStreamSynchronize(s));
+          CK(hipStreamSynchronize(s2));
+          best = std::min(best, ms_since(t0));
+        }
+        char ex[96];
+        snprintf(ex, sizeof ex, ", \"pieces\": %d, \"streams\": %d", pieces, streams);
+        rep("pageable_pieces", best, ex);
+      }
+    }
+    CK(hipStreamDestroy(s2));
+  }
   // pinned source
   char* pin;
   auto tp = clk::now();

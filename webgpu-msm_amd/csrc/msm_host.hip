@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -204,15 +205,26 @@ struct Slot {
   uint64_t seg_clock = 0;
   hipEvent_t ev_start = nullptr, ev_acc0 = nullptr, ev_acc1 = nullptr, ev_end = nullptr, ev_done = nullptr;
   hipEvent_t ev_in = nullptr;  // inputs of the slot's next launch are in place (uploads, caller's stream)
+  hipEvent_t ev_sc = nullptr;  // the scalars of the slot's next launch are in place (host uploads)
   Plan pl{};
   bool acc_timed = false;
 };
 constexpr int NSLOT = 4;      // at most this many launches in flight (one HIP stream each)
 constexpr int NCHUNK_EV = 8;  // events marking uploaded point chunks
 
+class TailCrew;
+
+// What the launch plans take from the device: compute units, and k_accumulate's waves per SIMD
+// (the occupancy query at context creation; run_length_for fills whole rounds of them).  The test
+// hooks plan for the defaults, so their plans do not depend on which device was used first.
+struct DevShape {
+  int n_cu = 256;
+  int acc_waves = 4;
+};
+
 struct DevCtx {
   int device = -1;
-  int n_cu = 256;
+  DevShape shape;
   std::mutex mu;
   Slot slot[NSLOT];
   hipStream_t copy_stream = nullptr;  // host->device uploads (overlap the slots' kernels)
@@ -229,6 +241,7 @@ struct DevCtx {
   hipEvent_t ev_base = nullptr;  // per-call time origin of the accumulation intervals (profiling 2)
   std::vector<std::pair<float, float>> acc_ivals;
   msm_profile_t last{};
+  TailCrew* crew = nullptr;  // a lone MSM's host-tail helpers (persistent, created on first use)
 };
 
 std::mutex g_mu;
@@ -236,7 +249,6 @@ std::vector<DevCtx*> g_ctx;   // indexed by HIP ordinal
 std::vector<int> g_gfx950;    // HIP ordinals of the gfx950 devices
 int g_nhip = -1;              // HIP devices visible (any architecture)
 std::atomic<int> g_profiling{0};  // read by calls on other devices' threads
-std::atomic<int> g_acc_waves{0};  // k_accumulate waves per SIMD (get_ctx's occupancy query)
 
 int probe_devices() {
   if (g_nhip >= 0) return (int)g_gfx950.size();
@@ -293,17 +305,18 @@ int get_ctx(int device, DevCtx** out) {
       hipEventCreate(&sl.ev_end);
       hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming);
+      hipEventCreateWithFlags(&sl.ev_sc, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_fork, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_join, hipEventDisableTiming);
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-      c->n_cu = prop.multiProcessorCount;
+      c->shape.n_cu = prop.multiProcessorCount;
     int acc_blocks = 0;  // k_accumulate workgroups per CU -> waves per SIMD (run_length_for)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&acc_blocks, reinterpret_cast<const void*>(&k_accumulate),
                                                      ACC_THREADS, 0) == hipSuccess &&
         acc_blocks > 0)
-      g_acc_waves.store(acc_blocks * (int)(ACC_THREADS / 64) / 4);
+      c->shape.acc_waves = std::max(1, acc_blocks * (int)(ACC_THREADS / 64) / 4);
     hipSetDevice(prev);
     g_ctx[device] = c;
   }
@@ -337,7 +350,8 @@ constexpr uint32_t RED1_LS[] = {8, 9, 10, 12, 16, 17, 20};
 // (profiles/r2i_ks17*): c = 15 with two MSMs per launch ran L = 8 as 1,056 waves -- two chains on
 // some SIMDs, 140 us -- where L = 9 fits.  Chains past 16 serve the four-MSM launches of small
 // sizes (2^17: L = 17, 994 waves).  MSM_RED_L overrides (any of RED1_LS, or 4).
-uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
+uint32_t bucket_reduce_L(const MsmDims& d, const DevShape& sh) {
+  const int n_cu = sh.n_cu;
   static const uint32_t l_env = getenv("MSM_RED_L") ? (uint32_t)atoi(getenv("MSM_RED_L")) : 0u;
   if (l_env == 4) return 4;
   for (uint32_t L : RED1_LS)
@@ -353,15 +367,9 @@ uint32_t bucket_reduce_L(const MsmDims& d, int n_cu) {
   return 16;
 }
 
-// Waves of k_accumulate one SIMD holds (4: VGPR- and LDS-bound), from the runtime's occupancy
-// query at the first device context (g_acc_waves).
-uint64_t acc_waves_per_simd() {
-  const int v = g_acc_waves.load();
-  return v > 0 ? (uint64_t)v : 4u;
-}
-
 // Run length K (entries per k_accumulate lane, a multiple of 4 for the 16-B entry loads): the
-// accumulation holds acc_waves_per_simd() waves per SIMD, so its lanes run in rounds of that
+// accumulation holds sh.acc_waves waves per SIMD (4: VGPR- and LDS-bound, from the runtime's
+// occupancy query for the device), so its lanes run in rounds of that
 // many x 4 x CUs waves, and a round only partly filled runs on few SIMDs for a full wave's time.
 // So K <= 64 (long enough to amortise the per-run joins) is chosen to fill whole rounds: the
 // fewest rounds r with K <= 64, then the smallest K that fits the launch's entries in r rounds
@@ -370,18 +378,19 @@ uint64_t acc_waves_per_simd() {
 // many runs a bucket spans: a bucket over 3 or more whole runs sends the launch through the skew
 // joins (§2.4 of DESIGN.md), so shorter runs than these cost a second reduction on random
 // scalars (a lone 2^20 MSM at K = 44: latency 1.16 -> 1.36 ms).
-uint32_t run_length_for(const MsmDims& d, int n_cu) {
+uint32_t run_length_for(const MsmDims& d, const DevShape& sh) {
   const uint64_t m = (uint64_t)d.nm * (d.Wm - 1) * d.n;
-  const uint64_t round_lanes = 64ull * acc_waves_per_simd() * 4 * (uint64_t)(n_cu > 0 ? n_cu : 256);
+  const uint64_t round_lanes =
+      64ull * (uint64_t)std::max(1, sh.acc_waves) * 4 * (uint64_t)(sh.n_cu > 0 ? sh.n_cu : 256);
   const uint64_t r = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
   uint64_t K = (m + r * round_lanes - 1) / (r * round_lanes);
   K = (K + 3) & ~3ull;
   return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, K));
 }
 
-int finish_plan(const MsmDims& d, const msm_opts* o, int n_cu, Plan* pl);
+int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl);
 
-int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = false, uint32_t nm = 1,
+int make_plan(size_t n, const msm_opts* o, const DevShape& sh, Plan* pl, bool pipelined = false, uint32_t nm = 1,
               bool shared = false) {
   *pl = Plan{};
   uint32_t c = (o && o->window_bits) ? o->window_bits : pipelined ? pipelined_window(n) : msm_best_window(n);
@@ -412,16 +421,16 @@ int make_plan(size_t n, const msm_opts* o, int n_cu, Plan* pl, bool pipelined = 
   d.nbins = d.W * d.nbc;
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
-  return finish_plan(d, o, n_cu, pl);
+  return finish_plan(d, o, sh, pl);
 }
 
 // The launch-shape fields that follow from the geometry d.
-int finish_plan(const MsmDims& d, const msm_opts* o, int n_cu, Plan* pl) {
+int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl) {
   const size_t n = d.n;
   pl->d = d;
-  pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, n_cu);
+  pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, sh);
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
-  pl->L = bucket_reduce_L(d, n_cu);
+  pl->L = bucket_reduce_L(d, sh);
   pl->nchunks = (d.B + pl->L - 1) / pl->L;
   // every k_bucket_reduce_2 workgroup sums at most pow2ceil(nchunks)/2 points (the R_k terms' size)
   pl->nv = pl->nchunks >= 2 ? 2 : 1;
@@ -707,16 +716,38 @@ int tail_helpers() {
 
 class TailCrew {
  public:
+  // The helpers are started once (per device context) and sleep between MSMs; arm() wakes them
+  // right after a launch so they spin (yielding) while the device works, and run() hands them the
+  // terms.  disarm() sends them back to sleep when no terms will come (an error return).
   explicit TailCrew(int helpers) {
     for (int i = 0; i < helpers; i++) th_.emplace_back([this] { work(); });
   }
   ~TailCrew() {
-    quit_.store(true);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_.store(true);
+    }
+    cv_.notify_all();
     for (std::thread& t : th_) t.join();
   }
   bool active() const { return !th_.empty(); }
+  void arm() {
+    if (th_.empty()) return;
+    wait_idle();  // the previous round is over (run() and disarm() wait for it too)
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      idle_.store(0);
+      armed_.store(true);
+      gen_++;
+    }
+    cv_.notify_all();
+  }
+  void disarm() {
+    armed_.store(false);
+    wait_idle();
+  }
   // The terms are on the host: the helpers start on the window sums, the caller on the outer
-  // Horner.
+  // Horner, taking each window sum as it becomes ready (and computing one itself when none is).
   Pt run(const Plan& pl, const uint32_t* terms) {
     pl_ = &pl;
     terms_ = terms;
@@ -726,10 +757,6 @@ class TailCrew {
     for (uint32_t w = 0; w < Wm; w++) ready_[w].store(0);
     next_.store(0);
     go_.store(true, std::memory_order_release);
-    std::vector<std::pair<uint32_t, const uint32_t*>> at;
-    for (uint32_t k = 0; k < Wm; k++) at.emplace_back(win_off(pl.d, Wm - 1 - k), nullptr);
-    // outer Horner over the window offsets; the window sums are taken as they become ready (the
-    // caller computes one itself when none is ready yet)
     Pt acc = pt_identity();
     bool any = false;
     for (uint32_t k = 0; k < Wm; k++) {
@@ -743,10 +770,17 @@ class TailCrew {
       const uint32_t next = w ? win_off(pl.d, w - 1) : 0u;
       if (any && win_off(pl.d, w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w) - next));
     }
+    // every helper is out of this job before its state is reset by the next one
+    armed_.store(false);
+    wait_idle();
+    go_.store(false);
     return acc;
   }
 
  private:
+  void wait_idle() {
+    while (idle_.load(std::memory_order_acquire) < (int)th_.size()) _mm_pause();
+  }
   // One window sum, top window first; false when none is left.
   bool take_one() {
     const uint32_t Wm = pl_->d.Wm;
@@ -760,17 +794,32 @@ class TailCrew {
     return true;
   }
   void work() {
-    uint64_t spins = 0;
-    while (!go_.load(std::memory_order_acquire)) {
-      if (quit_.load()) return;
-      if (++spins > 4096) std::this_thread::yield();  // a long device wait: stay cheap
-      else _mm_pause();
-    }
-    while (take_one()) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return quit_.load() || gen_ != seen; });
+        if (quit_.load()) return;
+        seen = gen_;
+      }
+      // armed: spin (a long device wait: stay cheap) until the terms are posted or the call ends
+      uint64_t spins = 0;
+      while (!go_.load(std::memory_order_acquire) && armed_.load() && !quit_.load()) {
+        if (++spins > 4096) std::this_thread::yield();
+        else _mm_pause();
+      }
+      if (go_.load(std::memory_order_acquire))
+        while (take_one()) {
+        }
+      idle_.fetch_add(1, std::memory_order_release);
     }
   }
   std::vector<std::thread> th_;
-  std::atomic<bool> go_{false}, quit_{false};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint64_t gen_ = 0;
+  std::atomic<bool> go_{false}, armed_{false}, quit_{false};
+  std::atomic<int> idle_{1 << 30};  // helpers done with the current round (all idle at start)
   std::atomic<uint32_t> next_{0};
   const Plan* pl_ = nullptr;
   const uint32_t* terms_ = nullptr;
@@ -1043,12 +1092,10 @@ int wait_event(hipStream_t s, hipEvent_t e) {
 }
 
 // Wait for the launch in slot `si` (spinning briefly: the result is usually due within a couple of
-// milliseconds, and a blocking wait adds a wake-up latency) and take its window terms.  With
-// `terms` the terms are copied out, so the slot can take its next launch before the host tail
-// runs; otherwise the host tail runs here, on the pinned buffer.
-// Wait for the launch in slot `si` and check its flags; its window terms are then in the slot's
-// h_out.  Skewed scalars: the sequence ran without the bucket joins (PART_JOIN), so they and the
-// reduction run again here (the slot's stream is idle: its next launch is enqueued afterwards).
+// milliseconds, and a blocking wait adds a wake-up latency) and check its flags; its window terms
+// are then in the slot's h_out.  Skewed scalars: the sequence ran without the bucket joins
+// (PART_JOIN), so they and the reduction run again here (the slot's stream is idle: its next launch
+// is enqueued afterwards).
 int wait_slot(DevCtx* c, int si, uint32_t* total_out = nullptr) {
   Slot& sl = c->slot[si];
   const Plan& pl = sl.pl;
@@ -1062,10 +1109,20 @@ int wait_slot(DevCtx* c, int si, uint32_t* total_out = nullptr) {
   const uint32_t err = h[outb / 4];
   if (total_out) *total_out = h[outb / 4 + 1];
   if (h[outb / 4 + 2]) {
-    if (int rc = enqueue_msm(c, pl, BatchPtrs{}, BatchPtrs{}, si, sl.stream, PART_JOIN | PART_POST, nullptr))
+    // only the second k_bucket_reduce_2 clears the skew list and the lead flag: if the re-run
+    // cannot be enqueued or does not complete, clear them here, or the slot's next MSM would append
+    // to a stale skew list and rejoin stale workgroups without any error
+    int rc = enqueue_msm(c, pl, BatchPtrs{}, BatchPtrs{}, si, sl.stream, PART_JOIN | PART_POST, nullptr);
+    if (rc == MSM_OK && (hipEventRecord(sl.ev_done, sl.stream) != hipSuccess ||
+                         hipEventSynchronize(sl.ev_done) != hipSuccess))
+      rc = MSM_ERR_HIP;
+    if (rc != MSM_OK) {
+      (void)hipGetLastError();
+      hipMemsetAsync(sl.ws.skew_list.p, 0, 4, sl.stream);
+      hipMemsetAsync(sl.ws.lead_flag.p, 0, sl.ws.lead_flag.cap, sl.stream);
+      hipStreamSynchronize(sl.stream);
       return rc;
-    HIPCHECK(hipEventRecord(sl.ev_done, sl.stream));
-    HIPCHECK(hipEventSynchronize(sl.ev_done));
+    }
   }
   if (err & MSM_DEV_ERR_COORD_RANGE) return MSM_ERR_COORD_RANGE;
   if (err & MSM_DEV_ERR_BAD_POINT) return MSM_ERR_BAD_POINT;
@@ -1167,6 +1224,16 @@ int order_after_user(DevCtx* c, hipStream_t user, int nslot) {
   return MSM_OK;
 }
 
+// The host tail of a lone MSM in slot `si`, over the device context's persistent helpers: armed
+// right after the launch (they spin while the device works), handed the terms when they land.
+int finish_lone(DevCtx* c, int si, Pt* result) {
+  if (!c->crew) c->crew = new TailCrew(tail_helpers());
+  c->crew->arm();
+  const int rc = finish_msm(c, si, result, nullptr, c->crew);
+  if (rc != MSM_OK) c->crew->disarm();  // no terms will come
+  return rc;
+}
+
 // Run one MSM with device inputs; result as a projective host point.
 int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, size_t n, const msm_opts* o,
                hipStream_t user_stream, Pt* result) {
@@ -1175,7 +1242,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
     return MSM_OK;
   }
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl);
+  int rc = make_plan(n, o, c->shape, &pl);
   if (rc != MSM_OK) return rc;
   const int si = 0;  // a lone MSM always uses slot 0 (the other workspaces only for pipelining)
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
@@ -1183,8 +1250,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   c->slot[si].pl = pl;
   if ((rc = launch_parts(c, pl, splat(d_points), splat(d_scalars), si, PART_ALL, c->slot[si].ws.pts.as<uint32_t>())))
     return rc;
-  TailCrew crew(tail_helpers());  // started after the launch: thread start-up overlaps the device
-  return finish_msm(c, si, result, nullptr, &crew);
+  return finish_lone(c, si, result);
 }
 
 // Host -> device copy of one input array on the copy stream, in pieces of `piece` bytes; after
@@ -1240,7 +1306,7 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
     return MSM_OK;
   }
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl);
+  int rc = make_plan(n, o, c->shape, &pl);
   if (rc != MSM_OK) return rc;
   const int si = 0;
   Slot& sl = c->slot[si];
@@ -1262,8 +1328,7 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
     return fail(rc);
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return fail(rc);
-  TailCrew crew(tail_helpers());
-  return finish_msm(c, si, result, nullptr, &crew);
+  return finish_lone(c, si, result);
 }
 
 // MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
@@ -1351,7 +1416,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       in.batch ? std::min<size_t>(in.batch, count) : pipeline_batch(n, count), MSM_MAX_BATCH);
   const size_t nbatch = (count + nm - 1) / nm;
   Plan pl;
-  int rc = make_plan(n, o, c->n_cu, &pl, count > 1, nm, shared);
+  int rc = make_plan(n, o, c->shape, &pl, count > 1, nm, shared);
   if (rc != MSM_OK) return rc;
   // host inputs: one more launch in flight, so its upload queues behind the running ones
   // (2^20 msm_compute 4.21 -> 4.05 ms with three, profiles/r2t_*; device inputs are best with two)
@@ -1367,7 +1432,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     }
   }
   if ((rc = order_after_user(c, user_stream, nslot)) != MSM_OK) return rc;
-  auto fail = [&](int code) {
+  auto fail0 = [&](int code) {  // before the uploader starts
     hipStreamSynchronize(c->copy_stream);
     for (int k = 0; k < nslot; k++) hipStreamSynchronize(c->slot[k].stream);
     return code;
@@ -1382,14 +1447,126 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       if ((rc = s0.ws.wire_pts.ensure(n * 128)) != MSM_OK) return rc;
       rc = upload_points(c, in.shared_points, n, s0.ws.wire_pts.as<uint32_t>(), pts_shared, s0.ws.err.as<uint32_t>(),
                          s0.stream);
-      if (rc != MSM_OK) return fail(rc);
+      if (rc != MSM_OK) return fail0(rc);
     } else {
       launch_prepare(in.shared_points, pts_shared, (uint32_t)n, s0.ws.err.as<uint32_t>(), prep_nt(n), s0.stream);
-      if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
+      if (hipGetLastError() != hipSuccess) return fail0(MSM_ERR_HIP);
     }
-    if (hipEventRecord(c->ev_shared, s0.stream) != hipSuccess) return fail(MSM_ERR_HIP);
+    if (hipEventRecord(c->ev_shared, s0.stream) != hipSuccess) return fail0(MSM_ERR_HIP);
     for (int si = 1; si < nslot; si++)
-      if (hipStreamWaitEvent(c->slot[si].stream, c->ev_shared, 0) != hipSuccess) return fail(MSM_ERR_HIP);
+      if (hipStreamWaitEvent(c->slot[si].stream, c->ev_shared, 0) != hipSuccess) return fail0(MSM_ERR_HIP);
+  }
+  // The inputs of launch j (per-MSM pointers, or the slot's wire buffers for host inputs) and the
+  // number of real (not padding) MSMs in it.
+  auto launch_inputs = [&](size_t j, BatchPtrs* bp, BatchPtrs* bs) -> uint32_t {
+    Slot& sl = c->slot[j % nslot];
+    const uint32_t nreal = (uint32_t)std::min<size_t>(nm, count - j * nm);
+    *bp = BatchPtrs{};
+    *bs = BatchPtrs{};
+    for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
+      const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
+      bp->p[m] = shared ? in.shared_points : in.points[b];
+      bs->p[m] = in.scalars[b];
+      if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
+        const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
+        bs->p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
+        if (!shared) bp->p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
+      }
+    }
+    return nreal;
+  };
+  // Host inputs of launch j into its slot's wire buffers, on the copy stream: the scalars, the
+  // device padding of short MSMs, an event on the scalars (ev_sc), the points, an event on all of
+  // them (ev_in).  MSMs whose host arrays are adjacent (the slices of run_host_split) go up in one
+  // copy per array: each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between
+  // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
+  // up alone and its tail is padded on the device.
+  auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
+    Slot& sl = c->slot[j % nslot];
+    BatchPtrs bp, bs;
+    const uint32_t nreal = launch_inputs(j, &bp, &bs);
+    auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
+    auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
+      for (uint32_t m0 = 0; m0 < nreal;) {
+        const size_t b0 = std::min(j * nm + m0, count - 1);
+        const uint32_t* h0 = src[b0];
+        uint32_t m1 = m0 + 1;
+        if (len_of(b0) == n)
+          while (m1 < nreal && len_of(j * nm + m1) == n && src[j * nm + m1] == h0 + (size_t)(m1 - m0) * n * per) m1++;
+        const size_t words = (m1 - m0 == 1 ? len_of(b0) : (size_t)(m1 - m0) * n) * per;
+        if (words && hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, words * 4, hipMemcpyHostToDevice,
+                                    c->copy_stream) != hipSuccess)
+          return false;
+        m0 = m1;
+      }
+      return true;
+    };
+    if (!up(in.scalars, bs, 8)) return MSM_ERR_HIP;
+    for (uint32_t m = 0; m < nreal && !shared; m++) {
+      const size_t len = len_of(std::min(j * nm + m, count - 1));
+      if (len < n) {
+        hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
+                           const_cast<uint32_t*>(bp.p[m]) + len * 32, const_cast<uint32_t*>(bs.p[m]) + len * 8,
+                           (uint32_t)(n - len));
+        if (hipGetLastError() != hipSuccess) return MSM_ERR_HIP;
+      }
+    }
+    HIPCHECK(hipEventRecord(sl.ev_sc, c->copy_stream));
+    scalars_done();
+    if (!shared && !up(in.points, bp, 32)) return MSM_ERR_HIP;
+    HIPCHECK(hipEventRecord(sl.ev_in, c->copy_stream));
+    return MSM_OK;
+  };
+  // With host inputs and more than one launch, a helper thread (the uploader) issues every
+  // launch's copies back to back while this thread enqueues the launches and runs the host tails:
+  // a pageable hipMemcpyAsync returns only once its data is staged, so copies issued from the
+  // launching thread left the copy engine idle for every graph launch and host tail between them
+  // (~120 us per launch, profiles/r4/e2e_timeline_before.txt).  A slot's wire buffers are rewritten
+  // only after its previous launch is done with them: the copy stream waits for that launch's
+  // ev_done, recorded once this thread has enqueued it (`enqueued`).
+  const bool uploader = host && nbatch > 1;
+  std::atomic<size_t> sc_ready{0}, up_ready{0}, enqueued{0};
+  std::atomic<int> up_rc{MSM_OK};
+  std::atomic<bool> up_stop{false};
+  std::thread up_th;
+  auto wait_for = [&](std::atomic<size_t>& v, size_t want) -> bool {  // false: the uploader failed
+    for (uint32_t spins = 0; v.load(std::memory_order_acquire) < want; spins++) {
+      if (up_rc.load() != MSM_OK) return false;
+      if (spins > 256) std::this_thread::yield();
+      else _mm_pause();
+    }
+    return true;
+  };
+  auto stop_uploader = [&] {
+    up_stop.store(true);
+    if (up_th.joinable()) up_th.join();
+  };
+  auto fail = [&](int code) {
+    stop_uploader();
+    hipStreamSynchronize(c->copy_stream);
+    for (int k = 0; k < nslot; k++) hipStreamSynchronize(c->slot[k].stream);
+    return code;
+  };
+  if (uploader) {
+    up_th = std::thread([&] {
+      hipSetDevice(c->device);
+      for (size_t j = 0; j < nbatch && !up_stop.load(); j++) {
+        int urc = MSM_OK;
+        if (j >= (size_t)nslot) {
+          // launch j - nslot (the slot's previous one) must have been enqueued before its
+          // ev_done can be waited for
+          while (enqueued.load(std::memory_order_acquire) < j - nslot + 1 && !up_stop.load()) std::this_thread::yield();
+          if (up_stop.load()) break;
+          if (hipStreamWaitEvent(c->copy_stream, c->slot[j % nslot].ev_done, 0) != hipSuccess) urc = MSM_ERR_HIP;
+        }
+        if (urc == MSM_OK) urc = upload_launch(j, [&] { sc_ready.store(j + 1, std::memory_order_release); });
+        if (urc != MSM_OK) {
+          up_rc.store(urc);
+          break;
+        }
+        up_ready.store(j + 1, std::memory_order_release);
+      }
+    });
   }
   // Launch j goes to slot j % nslot.  Its previous occupant, launch j - nslot, is waited for and
   // its window terms copied out just before; the host tail (window Horner) of launch j - nslot
@@ -1403,73 +1580,28 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     if (j < nbatch) {
       const int si = (int)(j % nslot);
       Slot& sl = c->slot[si];
-      BatchPtrs bp{}, bs{};
-      const uint32_t nreal = (uint32_t)std::min<size_t>(nm, count - j * nm);  // MSMs of this launch
-      for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
-        const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
-        bp.p[m] = shared ? in.shared_points : in.points[b];
-        bs.p[m] = in.scalars[b];
-        if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
-          const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
-          bs.p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
-          if (!shared) bp.p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
-        }
-      }
+      BatchPtrs bp, bs;
+      launch_inputs(j, &bp, &bs);
       const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
       uint32_t* pts = shared ? pts_shared : sl.ws.pts.as<uint32_t>();
+      // The last launch's bucket sort starts on its scalars while its points upload: the sort then
+      // leaves the call's tail (earlier launches overlap the next uploads anyway).
       const bool sort_early = host && !shared && j + 1 == nbatch && nbatch > 1 && host_sort_early();
       if (host) {
-        // this slot's previous launch has finished (above): its wire buffers are free.  MSMs whose
-        // host arrays are adjacent (the slices of run_host_split) go up in one copy per array:
-        // each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between transfers.
-        // The padding MSMs of a short last launch upload nothing.
-        // A short MSM (in.lens) goes up alone and its tail is padded on the device.
-        auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
-        auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
-          for (uint32_t m0 = 0; m0 < nreal;) {
-            const size_t b0 = std::min(j * nm + m0, count - 1);
-            const uint32_t* h0 = src[b0];
-            uint32_t m1 = m0 + 1;
-            if (len_of(b0) == n)
-              while (m1 < nreal && len_of(j * nm + m1) == n &&
-                     src[j * nm + m1] == h0 + (size_t)(m1 - m0) * n * per)
-                m1++;
-            const size_t words = (m1 - m0 == 1 ? len_of(b0) : (size_t)(m1 - m0) * n) * per;
-            if (words && hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, words * 4, hipMemcpyHostToDevice,
-                                        c->copy_stream) != hipSuccess)
-              return false;
-            m0 = m1;
-          }
-          return true;
-        };
-        if (!up(in.scalars, bs, 8)) return fail(MSM_ERR_HIP);
-        for (uint32_t m = 0; m < nreal && !shared; m++) {
-          const size_t len = len_of(std::min(j * nm + m, count - 1));
-          if (len < n) {
-            hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
-                               const_cast<uint32_t*>(bp.p[m]) + len * 32, const_cast<uint32_t*>(bs.p[m]) + len * 8,
-                               (uint32_t)(n - len));
-            if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
-          }
-        }
-        // The last launch's bucket sort starts on its scalars while its points upload: the sort
-        // then leaves the call's tail (earlier launches overlap the next uploads anyway, and an
-        // extra graph launch between their copies would only widen the copy engine's gaps).
+        if (!uploader && (rc = upload_launch(j, [] {})) != MSM_OK) return fail(rc);
         if (sort_early) {
-          if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
-              hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
-            return fail(MSM_ERR_HIP);
+          if (uploader && !wait_for(sc_ready, j + 1)) return fail(up_rc.load());
+          if (hipStreamWaitEvent(sl.stream, sl.ev_sc, 0) != hipSuccess) return fail(MSM_ERR_HIP);
           sl.pl = pl;
           if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
         }
-        if (!shared && !up(in.points, bp, 32)) return fail(MSM_ERR_HIP);
-        if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess ||
-            hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
-          return fail(MSM_ERR_HIP);
+        if (uploader && !wait_for(up_ready, j + 1)) return fail(up_rc.load());
+        if (hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess) return fail(MSM_ERR_HIP);
       }
       sl.pl = pl;
       if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
         return fail(rc);
+      enqueued.store(j + 1, std::memory_order_release);
     }
     if (have) {
       // the launch's window Horners side by side (one host thread per MSM): the last launch's are
@@ -1483,6 +1615,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       for (uint32_t m = 0; m < k; m++) emit(res[m], f * nm + m);
     }
   }
+  stop_uploader();  // its last copies were waited for by the last launch
   return MSM_OK;
 }
 
@@ -1536,22 +1669,43 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
 // overlaps all the compute but the last launch's; the partials are joined with G - 1 adds.  When
 // G does not divide n the last slice is short: it is padded on the device (identity points, zero
 // scalars) rather than run as a separate remainder MSM after the others.
+// Points per slice of the split's last launch (MSM_HOST_TAIL_LOG; 0 = no short tail slices): what
+// is left to compute once the last upload has landed is that launch's preparation, accumulation
+// and reduction, so the last launch is made short.
+size_t host_tail() {
+  static const size_t v = getenv("MSM_HOST_TAIL_LOG") ? (atoi(getenv("MSM_HOST_TAIL_LOG")) > 0
+                                                            ? (size_t)1 << atoi(getenv("MSM_HOST_TAIL_LOG")) : 0)
+                                                      : (size_t)1 << 15;
+  return v;
+}
+
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
-  const size_t G = std::min<size_t>(16, n / host_piece());
-  const size_t s = (n + G - 1) / G;  // slices of s points; only the last is short (for n >= 2^18)
+  // The body: Gb slices (a whole number of launches) of at most s points, balanced; then one
+  // launch of short tail slices of t points each.  Every slice is an MSM of s points to the
+  // pipelined entry (in.lens: a short slice is padded on the device with identity points and zero
+  // scalars, which add no bucket entries).
+  const uint32_t nmb = host_batch();
+  size_t t = host_tail();
+  if (t * nmb * 8 > n) t = 0;  // small MSMs: no tail launch
+  const size_t body = n - t * nmb;
+  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, body / host_piece()));
+  Gb = (Gb + nmb - 1) / nmb * nmb;
+  const size_t s = (body + Gb - 1) / Gb;
+  const size_t G = Gb + (t ? nmb : 0);
   std::vector<const uint32_t*> pp(G), ss(G);
   std::vector<size_t> lens(G);
   for (size_t g = 0; g < G; g++) {
-    pp[g] = points_be + g * s * 32;
-    ss[g] = scalars_be + g * s * 8;
-    lens[g] = g * s < n ? std::min(s, n - g * s) : 0;  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
+    const size_t off = g < Gb ? g * s : body + (g - Gb) * t;
+    pp[g] = points_be + off * 32;
+    ss[g] = scalars_be + off * 8;
+    lens[g] = g < Gb ? (g * s < body ? std::min(s, body - g * s) : 0) : t;  // 0 only for tiny overrides
   }
   ManyInputs in;
   in.kind = ManyInputs::HOST;
   in.points = pp.data();
   in.scalars = ss.data();
-  in.batch = host_batch();
+  in.batch = nmb;
   in.lens = lens.data();
   std::vector<Pt> part(G, pt_identity());
   int rc = run_many(c, in, s, G, o, nullptr, nullptr, true, part.data());
@@ -1818,7 +1972,8 @@ void msm_shutdown(void) {
       for (Segment& sg : sl.seg) sg.drop();
       sl.h_out.release();
       sl.h_out_dev = nullptr;
-      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in, sl.ev_fork, sl.ev_join})
+      for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in, sl.ev_sc, sl.ev_fork,
+                          sl.ev_join})
         if (e) hipEventDestroy(e);
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
@@ -1831,6 +1986,8 @@ void msm_shutdown(void) {
       hipStreamDestroy(sl.aux);
     }
     hipStreamDestroy(c->copy_stream);
+    delete c->crew;
+    c->crew = nullptr;
     hipSetDevice(prev);
   }
   for (DevCtx*& c : g_ctx) {
@@ -2139,15 +2296,31 @@ int msm_test_peer_state(int dev, int owner) {
 // The host tail of a lone MSM of n points (auto plan) on caller-supplied window terms (host
 // Montgomery X|Y|T|Z words, the layout k_bucket_reduce_2 writes): helpers = 0 runs horner_tail,
 // otherwise the TailCrew.  Affine result; *ms = the tail's wall time.
+// helpers < 0: one crew of -helpers threads over 40 rounds (the persistent crew of a device
+// context), every third round armed and disarmed without terms first (an error return); the
+// result of the last round, MSM_ERR_INVALID_ARG if any round disagrees with the first.
 int msm_test_tail(size_t n, const uint32_t* terms, int helpers, uint32_t out_xy_be[16], double* ms) {
   Plan pl;
-  if (int rc = make_plan(n, nullptr, 256, &pl)) return rc;
-  TailCrew crew(helpers);
+  if (int rc = make_plan(n, nullptr, DevShape{}, &pl)) return rc;
+  const int rounds = helpers < 0 ? 40 : 1;
+  TailCrew crew(helpers < 0 ? -helpers : helpers);
+  Pt first{}, r{};
+  bool same = true;
   const auto t0 = clk::now();
-  const Pt r = helpers ? crew.run(pl, terms) : horner_tail(pl, terms);
-  *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  for (int k = 0; k < rounds; k++) {
+    if (helpers < 0 && k % 3 == 1) {
+      crew.arm();
+      crew.disarm();
+    }
+    crew.arm();
+    r = helpers ? crew.run(pl, terms) : horner_tail(pl, terms);
+    crew.disarm();
+    if (k == 0) first = r;
+    same = same && fq_eq(fq_mul(r.X, first.Z), fq_mul(first.X, r.Z)) && fq_eq(fq_mul(r.Y, first.Z), fq_mul(first.Y, r.Z));
+  }
+  *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count() / rounds;
   pt_to_be_affine(r, out_xy_be);
-  return MSM_OK;
+  return same ? MSM_OK : MSM_ERR_INVALID_ARG;
 }
 
 // Host field / curve timings (ns per operation, dependent chains): what 0 = fq_mul, 1 = one
@@ -2195,7 +2368,7 @@ int msm_test_host_timing(int what, size_t iters, double* ns) {
 // The number of window-term words msm_test_tail reads for n points.
 size_t msm_test_tail_words(size_t n) {
   Plan pl;
-  if (make_plan(n, nullptr, 256, &pl)) return 0;
+  if (make_plan(n, nullptr, DevShape{}, &pl)) return 0;
   return (size_t)pl.d.W * pl.nterms * 32;
 }
 

@@ -946,188 +946,6 @@ __device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WOR
   }
 }
 
-#ifndef MSM_ACC_DMA
-#define MSM_ACC_DMA 0
-#endif
-// ---- k_accumulate with the gather one entry ahead, by LDS-DMA ----------------------------------
-// The record of entry pos+1 is fetched straight into LDS (global_load_lds_dwordx4: no VGPRs) while
-// the wave computes entry pos's mixed add, so the gather's latency (L2 / Infinity Cache, ~1-2k
-// cycles) hides behind a whole iteration (~6k cycles of issue) instead of stalling the wave at
-// every iteration's start.  Each wave owns a slot of ACC_PRE_LOADS x 1 KiB: load j of lane l lands
-// at slot[j][l] (LDS-DMA writes wave base + lane x 16 B), read back by ds_read_b128, conflict-free.
-// The run heads that acc_tile stages in LDS (36.9 KiB per workgroup) go to global memory here
-// (g_head[run], touched once per run), which frees the LDS for the slots: 28 KiB of records, 2 KiB
-// of double-buffered sorted entries and 1 KiB of head keys per workgroup, four workgroups (16
-// waves) per CU as before.  A head and a finished bucket are then
-// one store path to two addresses, where acc_tile had two divergent paths (global and LDS).
-constexpr uint32_t ACC_PRE_LOADS = 7;
-typedef __attribute__((address_space(3))) void lds_void;
-
-// LDS-DMA of the record of entry `ent` (point index << 1 | sign) into the wave's slot: the halves
-// in sign order, as load_pre_signed reads them (the half read first carries every top limb).
-__device__ __forceinline__ void gather_pre_lds(const uint32_t* __restrict__ pts, uint32_t ent, uint4* slot) {
-  const char* rec = reinterpret_cast<const char*>(pts) + ((size_t)(ent & ~1u) << 6);
-  const uint32_t o0 = (ent & 1u) * (PRE_HALF * 4);
-  const char* h0 = rec + o0;
-  const char* h1 = rec + (o0 ^ (PRE_HALF * 4));
-  const char* kt = rec + PRE_KT * 4;
-  __builtin_amdgcn_global_load_lds(h0, (lds_void*)(slot + 0 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(h0 + 16, (lds_void*)(slot + 1 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(h0 + 32, (lds_void*)(slot + 2 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(h1, (lds_void*)(slot + 3 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(h1 + 16, (lds_void*)(slot + 4 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(kt, (lds_void*)(slot + 5 * 64), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(kt + 16, (lds_void*)(slot + 6 * 64), 16, 0, 0);
-}
-
-// The record staged by gather_pre_lds, read by lane `lane` and decoded as load_pre_signed does.
-__device__ __forceinline__ void read_pre_lds(const uint4* slot, uint32_t lane, uint4 r[ACC_PRE_LOADS]) {
-#pragma unroll
-  for (uint32_t j = 0; j < ACC_PRE_LOADS; j++) r[j] = slot[j * 64 + lane];
-}
-__device__ __forceinline__ pre decode_pre(const uint4 r[ACC_PRE_LOADS], bool neg) {
-  const uint32_t av[NL] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w, r[2].x};
-  const uint32_t bv[NL] = {r[3].x, r[3].y, r[3].z, r[3].w, r[4].x, r[4].y, r[4].z, r[4].w, r[2].z};
-  const uint32_t kv[NL] = {r[5].x, r[5].y, r[5].z, r[5].w, r[6].x, r[6].y, r[6].z, r[6].w, r[2].y};
-  pre q;
-#pragma unroll
-  for (int k = 0; k < NL; k++) {
-    q.ymx.v[k] = av[k];
-    q.ypx.v[k] = bv[k];
-    q.kt.v[k] = kv[k];
-  }
-  q.kt = kt_neg_if(q.kt, neg);
-  return q;
-}
-
-__device__ __forceinline__ void acc_tile_dma(uint32_t wg, uint4* slot, uint4* ebuf, uint32_t* sh_hkey,
-                                             const uint32_t* __restrict__ pts,
-                                             const uint32_t* __restrict__ sorted_entry,
-                                             const uint32_t* __restrict__ bucket_start,
-                                             const uint32_t* __restrict__ run_key,
-                                             const uint32_t* __restrict__ total_ptr, uint32_t K, uint32_t nkeys,
-                                             uint32_t* __restrict__ buckets, uint32_t* __restrict__ lead_val,
-                                             uint32_t* __restrict__ lead_open, uint32_t* __restrict__ cross_key,
-                                             uint32_t* __restrict__ skew_list, uint32_t* __restrict__ g_head,
-                                             uint32_t* __restrict__ g_hkey, uint32_t* __restrict__ g_tkey) {
-  const uint32_t M = *total_ptr;
-  const uint32_t lt = threadIdx.x;
-  const uint32_t lane = lt & 63;
-  const uint32_t t = wg * ACC_THREADS + lt;
-  const uint32_t s = t * K;
-  uint32_t* my_head = g_head + (size_t)t * PT_WORDS;
-  sh_hkey[lt] = KEY_INVALID;
-  xyzt acc = pt_identity();
-  uint32_t cur = KEY_INVALID;
-  bool has_tail = false, cont = false;
-  if (s < M) {
-    const uint32_t e = min(s + K, M);
-    cur = run_key[t];
-    const bool started_before = bucket_start[cur] < s;
-    uint32_t bend = bucket_start[cur + 1];   // end of bucket `cur`
-    uint32_t bnext = bucket_start[cur + 2];  // end of the bucket after it (prefetched)
-    bool seg_first = true;
-    // Sorted entries four at a time (K is a multiple of 4, so runs are 16-B aligned), by LDS-DMA as
-    // well (no VGPRs held across iterations): group g = entries [s + 4g, +4) lands in the wave's
-    // entry buffer g & 1, fetched at the start of group g - 1; each iteration reads the one entry
-    // it needs next with a ds_read_b32.
-    uint32_t ent_cur = sorted_entry[s];
-    __builtin_amdgcn_global_load_lds(sorted_entry + s, (lds_void*)(ebuf), 16, 0, 0);
-    gather_pre_lds(pts, ent_cur, slot);
-    for (uint32_t pos = s; pos < e; pos++) {
-      const uint32_t it = pos - s;  // uniform across the lanes still in the loop
-      const uint32_t jq = it & 3u;
-      if (pos == bend) {
-        // a finished piece: the run's head (the end of a bucket begun in an earlier run) or a
-        // whole bucket -- one store, two addresses
-        const bool head = seg_first && started_before;
-        store_pt(head ? my_head : buckets + (size_t)cur * PT_WORDS, acc);
-        if (head) sh_hkey[lt] = cur;
-        // advance to the next non-empty bucket (a run of empty ones is skipped by galloping)
-        cur++;
-        bend = bnext;
-        bnext = bucket_start[cur + 2];
-        if (bend == pos) {
-          cur = next_nonempty(bucket_start, cur, pos, nkeys);
-          bend = bucket_start[cur + 1];
-          bnext = bucket_start[cur + 2];
-        }
-        acc = pt_identity();
-        seg_first = false;
-      }
-      // the next entry (its record is fetched during this iteration's add)
-      const bool more = pos + 1 < e;
-      uint32_t ent_nxt = 0;
-      if (more) ent_nxt = reinterpret_cast<const uint32_t*>(ebuf + (((it + 1) >> 2) & 1u) * 64 + lane)[(it + 1) & 3u];
-      // this entry's record: staged by the previous iteration's DMA (the wave's vmcnt covers it)
-      uint4 r[ACC_PRE_LOADS];
-      read_pre_lds(slot, lane, r);
-      // the slot is rewritten by the next DMA only after every lane's reads have returned (WAR)
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) gather_pre_lds(pts, ent_nxt, slot);
-      // group g + 1's entries into buffer (g + 1) & 1 (last read two iterations ago)
-      if (jq == 0 && pos + 4 < e)
-        __builtin_amdgcn_global_load_lds(sorted_entry + pos + 4, (lds_void*)(ebuf + (((it >> 2) + 1) & 1u) * 64), 16,
-                                         0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      const pre q = decode_pre(r, (ent_cur & 1u) != 0);
-      ent_cur = ent_nxt;
-      acc = pt_madd(acc, q);
-    }
-    cont = bend > e;  // bucket `cur` continues into the next run
-    if (seg_first && started_before) {  // the whole run belongs to a bucket begun earlier
-      store_pt(my_head, acc);
-      sh_hkey[lt] = cur | (cont ? KEY_PASS : 0u);
-    } else if (cont) {
-      has_tail = true;  // acc = tail piece of bucket `cur`
-    } else {
-      store_pt(buckets + (size_t)cur * PT_WORDS, acc);
-    }
-  }
-  // the last live run of the workgroup says whether a bucket leaves the workgroup
-  const uint32_t nruns = (M + K - 1) / K;
-  const uint32_t last = min(ACC_THREADS, nruns - min(nruns, wg * ACC_THREADS)) - 1;
-  if (lt == last) cross_key[wg] = cont ? cur : KEY_INVALID;
-  __syncthreads();  // the heads (global) and their keys (LDS) are visible to the workgroup
-  const uint32_t hk = sh_hkey[lt];
-  auto is_pass = [&](uint32_t r) {
-    const uint32_t k = sh_hkey[r];
-    return k != KEY_INVALID && (k & KEY_PASS) != 0;
-  };
-  const bool my_pass = hk != KEY_INVALID && (hk & KEY_PASS);
-  const bool nxt_pass = lt < last && is_pass(lt + 1);
-  const bool nxt2_pass = lt + 1 < last && is_pass(lt + 2);
-  const uint32_t* heads = g_head + (size_t)wg * ACC_THREADS * PT_WORDS;  // head of lane r: heads + r * 36
-  if (__syncthreads_or((my_pass && nxt_pass && nxt2_pass) ||
-                       (lt == 0 && my_pass && (last == 0 || (nxt_pass && last == 1))))) {
-    // skewed workgroup: heads (already in g_head) and tail pieces for k_chain_join
-    if (s < M) {
-      g_hkey[t] = hk;
-      g_tkey[t] = has_tail ? cur : KEY_INVALID;
-      if (has_tail) store_pt(buckets + (size_t)cur * PT_WORDS, acc);
-    }
-    if (lt == 0) skew_list[1 + atomicAdd(&skew_list[0], 1u)] = wg;
-    return;
-  }
-  const bool lead_join = lt == 0 && my_pass;
-  if (lt == 0) {
-    lead_open[wg] = 0u;
-    if (s < M && hk != KEY_INVALID && !lead_join) store_pt(lead_val + (size_t)wg * PT_WORDS, load_pt(heads));
-  }
-  if (has_tail || lead_join) {
-    const uint32_t nwalk =
-        lead_join ? 1u + (nxt_pass ? 1u : 0u)
-                  : (lt < last ? 1u + ((nxt_pass && lt + 1 < last) ? 1u + ((nxt2_pass && lt + 2 < last) ? 1u : 0u) : 0u)
-                               : 0u);
-    if (lead_join) acc = load_pt(heads);
-    if (nwalk) acc = pt_add(acc, load_pt(heads + (size_t)(lt + 1) * PT_WORDS));
-    if (nwalk > 1) acc = pt_add(acc, load_pt(heads + (size_t)(lt + 2) * PT_WORDS));
-    if (nwalk > 2) acc = pt_add(acc, load_pt(heads + (size_t)(lt + 3) * PT_WORDS));
-    store_pt(lead_join ? lead_val + (size_t)wg * PT_WORDS : buckets + (size_t)cur * PT_WORDS, acc);
-  }
-}
-
 // The kernel: one tile per workgroup.  (A persistent grid of 2-3 workgroups per CU striding over
 // the tiles, to leave CU room for the other launch's kernels, measured no faster: DESIGN.md §4.1.)
 extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uint32_t* __restrict__ pts,
@@ -1144,20 +962,10 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
                                          uint32_t* __restrict__ g_head,
                                          uint32_t* __restrict__ g_hkey,
                                          uint32_t* __restrict__ g_tkey) {
-#if MSM_ACC_DMA
-  __shared__ uint4 sh_pre[ACC_THREADS / 64][ACC_PRE_LOADS * 64];
-  __shared__ uint4 sh_ent[ACC_THREADS / 64][2 * 64];
-  __shared__ uint32_t sh_hkey[ACC_THREADS];
-  // the wave's slots: a wave-uniform (SGPR) base, so every LDS-DMA's M0 is a scalar add
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  acc_tile_dma(blockIdx.x, sh_pre[wv], sh_ent[wv], sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K,
-               nkeys, buckets, lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
-#else
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
   __shared__ uint32_t sh_hkey[ACC_THREADS];
   acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets,
            lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
-#endif
 }
 
 // Joins for workgroups that k_accumulate found to hold a pass-through run (skewed scalars).

@@ -27,6 +27,7 @@
 #include <node_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -47,12 +48,21 @@ namespace {
 
 // Staging for the copies of plain-ArrayBuffer inputs: one buffer pair kept between calls (its pages
 // stay mapped: a fresh 160 MB allocation per 2^20 call spent ~60 ms in first-touch page faults),
-// lent to one job at a time; a concurrent job gets its own.
+// lent to one job at a time; a concurrent job gets its own and frees it when done.  The cached pair
+// is kept only up to MSM_NODE_STAGING_CACHE_MB (default 256 MiB: a 2^20 MSM's 160 MiB); a larger
+// one is freed after its job.  SharedArrayBuffer inputs need no staging at all.
 struct Staging {
   std::vector<uint32_t> points, scalars;
+  size_t bytes() const { return (points.capacity() + scalars.capacity()) * 4; }
 };
 std::mutex g_stage_mu;
 Staging* g_stage = nullptr;  // the idle cached pair, or null while lent out
+
+size_t staging_cache_cap() {
+  static const size_t cap = (getenv("MSM_NODE_STAGING_CACHE_MB") ? (size_t)atol(getenv("MSM_NODE_STAGING_CACHE_MB"))
+                                                                  : (size_t)256) << 20;
+  return cap;
+}
 
 Staging* take_staging() {
   std::lock_guard<std::mutex> lk(g_stage_mu);
@@ -62,7 +72,7 @@ Staging* take_staging() {
 }
 void give_staging(Staging* s) {
   std::lock_guard<std::mutex> lk(g_stage_mu);
-  if (!g_stage) {
+  if (!g_stage && s->bytes() <= staging_cache_cap()) {
     g_stage = s;
   } else {
     delete s;

@@ -84,10 +84,13 @@ def load() -> ctypes.CDLL:
     # its libraries NEED by the unversioned name.  Loading torch first lets libmsm bind to that
     # same runtime by soname; loading libmsm first would pull /opt/rocm's copy and torch would
     # then initialise a second runtime that sees no devices.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # (MSM_AMD_NO_TORCH=1 skips this: libmsm then runs on /opt/rocm's runtime, as the Node addon and
+    # C callers do -- for comparing the two runtimes)
+    if not os.environ.get("MSM_AMD_NO_TORCH"):
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(_LIB)
     u32p = ctypes.POINTER(ctypes.c_uint32)
     vp = ctypes.c_void_p
