@@ -40,6 +40,7 @@ extern "C" {
 /* msm_opts.flags */
 #define MSM_FLAG_SERIAL 1u  /* pipelined entries: one launch in flight at a time (no overlap)     */
 #define MSM_FLAG_DEVICES 2u /* the device-list fields (devices, n_devices) are set: see below     */
+#define MSM_FLAG_WINDOWS 4u /* the window-range fields (window_lo, window_hi) are set: see below  */
 
 #define MSM_MAX_DEVICES 16
 
@@ -71,7 +72,20 @@ typedef struct msm_opts {
   const int32_t* devices; /* n_devices HIP ordinals                                                */
   uint32_t n_devices;
   uint32_t reserved; /* 0 */
+  /* --- read only when flags & MSM_FLAG_WINDOWS --- */
+  uint32_t window_lo, window_hi; /* the MSM's windows [window_lo, window_hi) only (below)             */
 } msm_opts;
+
+/* Window range (MSM_FLAG_WINDOWS): with an explicit window_bits c, the scalars are recoded into
+ * msm_window_count(c) signed-digit windows (counted from the least significant; the last is the
+ * overflow window for bits 254..255 and the carry) and only windows [window_lo, window_hi) are
+ * sorted, accumulated and reduced: the result is sum over those windows w of 2^(offset w) G_w.
+ * The ranges of a partition of [0, msm_window_count(c)) sum (as group elements) to the whole MSM,
+ * so the window ranges are a second way to shard one MSM over devices besides the point vector:
+ * every device then reads all n points and scalars but does 1/D of the bucket work and of the
+ * reduction.  Meant for the *_partial entries; window_bits 0, an empty range or one
+ * past the last window give MSM_ERR_INVALID_ARG. */
+uint32_t msm_window_count(uint32_t window_bits);
 
 /* Per-phase device times (ms) of the most recent MSM on the calling thread's device when
  * profiling is enabled (hipEvents on the library's stream). */

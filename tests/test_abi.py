@@ -120,12 +120,16 @@ def test_opts_struct_layout_matches_header():
     """msm_opts: the original 16-byte layout, then the device list (include/msm.h)."""
     src = open(HEADER).read()
     body = src[src.index("typedef struct msm_opts {"):src.index("} msm_opts;")]
-    fields = re.findall(r"^\s*(?:const\s+)?([a-z0-9_]+\*?)\s*(\*?)([a-z_]+);", body, flags=re.M)
-    assert [f[2] for f in fields] == [n for n, _ in M.MsmOpts._fields_]
-    assert ctypes.sizeof(M.MsmOpts) == 32
+    names = []
+    for decl in re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\s*\*?\s*([a-z_][a-z_, ]*);", body, flags=re.M):
+        names += [x.strip() for x in decl.split(",")]
+    assert names == [n for n, _ in M.MsmOpts._fields_]
+    assert ctypes.sizeof(M.MsmOpts) == 40
     assert M.MsmOpts.devices.offset == 16 and M.MsmOpts.n_devices.offset == 24
+    assert M.MsmOpts.window_lo.offset == 32 and M.MsmOpts.window_hi.offset == 36
     flags = dict(re.findall(r"#define (MSM_FLAG_[A-Z]+) (\d+)u", src))
     assert int(flags["MSM_FLAG_SERIAL"]) == M.MSM_FLAG_SERIAL and int(flags["MSM_FLAG_DEVICES"]) == M.MSM_FLAG_DEVICES
+    assert int(flags["MSM_FLAG_WINDOWS"]) == M.MSM_FLAG_WINDOWS
     assert int(re.search(r"#define MSM_MAX_DEVICES (\d+)", src).group(1)) == M.MSM_MAX_DEVICES
 
 
@@ -160,3 +164,12 @@ def test_device_ordinals_consistent():
         with pytest.raises(M.MsmError) as e:
             M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]), devices=[0])
         assert e.value.code == -6
+
+
+def test_window_count():
+    """msm_window_count: balanced main windows over scalar bits [0, 254) plus the overflow window
+    (DESIGN.md §2); 0 for an unsupported width."""
+    L = M.load()
+    for c in range(4, 21):
+        assert L.msm_window_count(c) == -(-254 // c) + 1 == M.window_count(c)
+    assert L.msm_window_count(16) == 17 and L.msm_window_count(0) == 0 and L.msm_window_count(21) == 0

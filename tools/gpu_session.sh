@@ -18,6 +18,7 @@
 #   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
+#   split        per-GPU work of every points x windows split of a 2^20 MSM over 8 GPUs, on this one
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
 #   kstats1      the same on one stream, kernels in order (MSM_SLOTS=1 MSM_FORK_PREP=0), two-MSM 2^20
 #                launches only (the serial pass warms the GPU first, so the trace averages the
@@ -113,6 +114,7 @@ for step in "$@"; do
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 2 \
         --no-extras "${BENCH_Q[@]}" ;;
     multidev) run multidev 300 python bench.py --multi-device --no-extras "${BENCH_Q[@]}" ;;
+    split) run split 600 python tools/split_probe.py --gpus 8 ;;
     kstats)
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;

@@ -23,8 +23,10 @@ struct MsmDims {
   uint32_t n;      // points per MSM
   uint32_t c;      // widest window (bits); digit codes and bucket tables are sized for it
   uint32_t B;      // buckets per window = 2^(c-1) (signed digits; narrower windows use fewer)
-  uint32_t W;      // windows of the whole batch = nm * Wm
-  uint32_t Wm;     // windows per MSM, overflow window included
+  uint32_t W;      // windows of the whole batch = nm * Wr
+  uint32_t Wm;     // windows per MSM, overflow window included (all of them are recoded)
+  uint32_t w0;     // window range of this launch (msm_opts MSM_FLAG_WINDOWS): windows
+  uint32_t Wr;     //   [w0, w0 + Wr) of every MSM; local window l of an MSM is window w0 + l
   uint32_t nm;     // MSMs in the batch
   uint32_t q;      // main-window base width
   uint32_t nhi;    // main windows of width q + 1
@@ -43,7 +45,8 @@ struct MsmDims {
 constexpr uint32_t MAIN_BITS = 254;  // bits covered by the main windows (scalars < 2^253, + carry)
 constexpr uint32_t OVF_BITS = 3;     // overflow window: bits 254, 255 and the carry (digit <= 4)
 
-// Width and bit offset of window w (w < Wm: a window of one MSM).
+// Width and bit offset of window w (w < Wm: a window of one MSM, counted from the least
+// significant; a launch's local window l is window d.w0 + l).
 __host__ __device__ inline uint32_t win_bits(const MsmDims& d, uint32_t w) {
   return w + 1 == d.Wm ? OVF_BITS : (w < d.nhi ? d.q + 1 : d.q);
 }

@@ -133,7 +133,8 @@ struct Plan {
 // replayed only for an identical plan.
 bool plan_eq(const Plan& a, const Plan& b) {
   const MsmDims &x = a.d, &y = b.d;
-  return x.n == y.n && x.c == y.c && x.B == y.B && x.W == y.W && x.Wm == y.Wm && x.nm == y.nm && x.q == y.q &&
+  return x.n == y.n && x.c == y.c && x.B == y.B && x.W == y.W && x.Wm == y.Wm && x.w0 == y.w0 && x.Wr == y.Wr &&
+         x.nm == y.nm && x.q == y.q &&
          x.nhi == y.nhi && x.fb == y.fb && x.nbc == y.nbc && x.nbins == y.nbins && x.ch == y.ch && x.nch == y.nch &&
          x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L &&
          a.nchunks == b.nchunks && a.nv == b.nv && a.nterms == b.nterms && a.Mmax == b.Mmax &&
@@ -232,6 +233,7 @@ struct DevCtx {
   hipEvent_t ev_user = nullptr;  // recorded on a caller's stream: the library's streams wait on it
   hipEvent_t ev_shared = nullptr;
   Buf shared_pts;  // point records of a shared base vector (msm_compute_shared*)
+  Buf host_sc;     // all the scalars of a split host-input MSM (run_host_split), uploaded first
   hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
   int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate + device total per launch
   // The launch sequence of each slot is captured into HIP graphs and replayed: one
@@ -356,12 +358,12 @@ uint32_t bucket_reduce_L(const MsmDims& d, const DevShape& sh) {
   if (l_env == 4) return 4;
   for (uint32_t L : RED1_LS)
     if (l_env == L) return L;
-  const uint32_t nmain = d.Wm - 1;
-  const uint32_t nfull = d.nhi ? d.nhi : nmain;
   const uint64_t simds = 4ull * (uint64_t)(n_cu > 0 ? n_cu : 256);
   for (uint32_t L : RED1_LS) {
-    const uint64_t lc_hi = (d.B + L - 1) / L, lc_lo = d.nhi ? (d.B / 2 + L - 1) / L : lc_hi;
-    const uint64_t lanes = (uint64_t)d.nm * (nfull * lc_hi + (nmain - nfull) * lc_lo);
+    const uint32_t nchunks = (d.B + L - 1) / L;
+    uint64_t lanes = 0;
+    for (uint32_t l = 0; l < d.Wr; l++) lanes += red1_live_chunks(d, L, nchunks, d.w0 + l);
+    lanes *= d.nm;
     if ((lanes + 63) / 64 <= simds) return L;
   }
   return 16;
@@ -379,7 +381,9 @@ uint32_t bucket_reduce_L(const MsmDims& d, const DevShape& sh) {
 // joins (§2.4 of DESIGN.md), so shorter runs than these cost a second reduction on random
 // scalars (a lone 2^20 MSM at K = 44: latency 1.16 -> 1.36 ms).
 uint32_t run_length_for(const MsmDims& d, const DevShape& sh) {
-  const uint64_t m = (uint64_t)d.nm * (d.Wm - 1) * d.n;
+  // main windows of the launch's range (the overflow window holds no entry for canonical scalars)
+  const uint64_t nmain = d.Wr - ((d.w0 + d.Wr == d.Wm) ? 1u : 0u);
+  const uint64_t m = (uint64_t)d.nm * std::max<uint64_t>(1, nmain) * d.n;
   const uint64_t round_lanes =
       64ull * (uint64_t)std::max(1, sh.acc_waves) * 4 * (uint64_t)(sh.n_cu > 0 ? sh.n_cu : 256);
   const uint64_t r = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
@@ -405,7 +409,15 @@ int make_plan(size_t n, const msm_opts* o, const DevShape& sh, Plan* pl, bool pi
   d.nhi = MAIN_BITS - d.q * wm;
   d.Wm = wm + 1;
   d.nm = nm;
-  d.W = d.Wm * nm;
+  d.w0 = 0;
+  d.Wr = d.Wm;
+  if (o && (o->flags & MSM_FLAG_WINDOWS)) {
+    // a window range needs an explicit width, so that every caller's ranges cut the same windows
+    if (!o->window_bits || o->window_lo >= o->window_hi || o->window_hi > d.Wm) return MSM_ERR_INVALID_ARG;
+    d.w0 = o->window_lo;
+    d.Wr = o->window_hi - o->window_lo;
+  }
+  d.W = d.Wr * nm;
   d.c = d.nhi ? d.q + 1 : d.q;
   d.B = 1u << (d.c - 1);
   // Coarse bins: aim at ~4K entries per bin (half the LDS staging capacity of k_fine_sort) with at
@@ -562,7 +574,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
       mark(PH_START);
       mark(PH_PREPARE);
     }
-    const size_t hist_lds = (size_t)d.Wm * d.nbc * 4;
+    const size_t hist_lds = (size_t)d.Wr * d.nbc * 4;
     const unsigned rc_grid = grid_for(d.n, RC_SPAN);
     if (d.c <= 16) {
       hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
@@ -654,8 +666,9 @@ Pt term_at(const uint32_t* o) {
   return p;
 }
 
-// (bit position - base, term) pairs of windows [w0, w1) of MSM terms block `terms`: V slices at
-// the window's offset, R_k once per set bit b of L at offset + k + b; identity terms skipped.
+// (bit position - base, term) pairs of the launch's local windows [w0, w1) of MSM terms block
+// `terms` (local window l is window d.w0 + l of the MSM): V slices at the window's offset, R_k once
+// per set bit b of L at offset + k + b; identity terms skipped.
 void collect_terms(const Plan& pl, const uint32_t* terms, uint32_t w0, uint32_t w1, uint32_t base,
                    std::vector<std::pair<uint32_t, const uint32_t*>>* at) {
   const MsmDims& d = pl.d;
@@ -665,7 +678,7 @@ void collect_terms(const Plan& pl, const uint32_t* terms, uint32_t w0, uint32_t 
       Fq X;
       memcpy(X.l, o, 32);
       if (fq_is_zero(X) && !memcmp(o + 8, o + 24, 32)) continue;  // identity: X = 0, Y = Z
-      const uint32_t off = win_off(d, w) - base;
+      const uint32_t off = win_off(d, d.w0 + w) - base;
       if (t < pl.nv) {
         at->emplace_back(off, o);
       } else {
@@ -694,10 +707,10 @@ Pt horner_run(std::vector<std::pair<uint32_t, const uint32_t*>>& at, Get&& get) 
 
 Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
   const MsmDims& d = pl.d;
-  terms += (size_t)m * d.Wm * pl.nterms * 32;  // MSM m's windows
+  terms += (size_t)m * d.Wr * pl.nterms * 32;  // MSM m's windows
   std::vector<std::pair<uint32_t, const uint32_t*>> at;
-  at.reserve((size_t)d.Wm * pl.nterms * 2);
-  collect_terms(pl, terms, 0, d.Wm, 0, &at);
+  at.reserve((size_t)d.Wr * pl.nterms * 2);
+  collect_terms(pl, terms, 0, d.Wr, 0, &at);
   return horner_run(at, term_at);
 }
 
@@ -751,24 +764,24 @@ class TailCrew {
   Pt run(const Plan& pl, const uint32_t* terms) {
     pl_ = &pl;
     terms_ = terms;
-    const uint32_t Wm = pl.d.Wm;
-    sums_.assign(Wm, pt_identity());
-    ready_.reset(new std::atomic<int>[Wm]);
-    for (uint32_t w = 0; w < Wm; w++) ready_[w].store(0);
+    const uint32_t Wr = pl.d.Wr, w0 = pl.d.w0;  // local window w is window w0 + w of the MSM
+    sums_.assign(Wr, pt_identity());
+    ready_.reset(new std::atomic<int>[Wr]);
+    for (uint32_t w = 0; w < Wr; w++) ready_[w].store(0);
     next_.store(0);
     go_.store(true, std::memory_order_release);
     Pt acc = pt_identity();
     bool any = false;
-    for (uint32_t k = 0; k < Wm; k++) {
-      const uint32_t w = Wm - 1 - k;
+    for (uint32_t k = 0; k < Wr; k++) {
+      const uint32_t w = Wr - 1 - k;
       while (!ready_[w].load(std::memory_order_acquire))
         if (!take_one()) _mm_pause();
       const Pt& p = sums_[w];
       const bool ident = fq_is_zero(p.X) && fq_eq(p.Y, p.Z);
       if (!ident) acc = any ? pt_add(acc, p) : p;
       any = any || !ident;
-      const uint32_t next = w ? win_off(pl.d, w - 1) : 0u;
-      if (any && win_off(pl.d, w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w) - next));
+      const uint32_t next = w ? win_off(pl.d, w0 + w - 1) : 0u;
+      if (any && win_off(pl.d, w0 + w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w0 + w) - next));
     }
     // every helper is out of this job before its state is reset by the next one
     armed_.store(false);
@@ -783,12 +796,12 @@ class TailCrew {
   }
   // One window sum, top window first; false when none is left.
   bool take_one() {
-    const uint32_t Wm = pl_->d.Wm;
+    const uint32_t Wr = pl_->d.Wr;
     const uint32_t k = next_.fetch_add(1);
-    if (k >= Wm) return false;
-    const uint32_t w = Wm - 1 - k;
+    if (k >= Wr) return false;
+    const uint32_t w = Wr - 1 - k;
     std::vector<std::pair<uint32_t, const uint32_t*>> at;
-    collect_terms(*pl_, terms_, w, w + 1, win_off(pl_->d, w), &at);
+    collect_terms(*pl_, terms_, w, w + 1, win_off(pl_->d, pl_->d.w0 + w), &at);
     sums_[w] = horner_run(at, term_at);
     ready_[w].store(1, std::memory_order_release);
     return true;
@@ -1167,7 +1180,7 @@ int finish_msm(DevCtx* c, int si, Pt* result, std::vector<uint32_t>* terms = nul
     P.host_tail = std::chrono::duration<float, std::milli>(t1 - t0).count();
     P.entries = total;
     P.window_bits = pl.d.c;
-    P.windows = pl.d.Wm;
+    P.windows = pl.d.Wr;
     P.run_length = pl.K;
     P.chunk_len = pl.L;
     P.msms_per_launch = pl.d.nm;
@@ -1382,6 +1395,8 @@ struct ManyInputs {
   uint32_t batch = 0;                        // MSMs per launch (0: pipeline_batch's choice)
   const size_t* lens = nullptr;  // host inputs: real points per MSM (<= n; the rest is padded on
                                  // the device with identity points and zero scalars); null: all n
+  const uint32_t* const* dev_scalars = nullptr;  // host inputs whose scalars are already on the
+                                                 // device (n + padding words per MSM): no scalar upload
 };
 
 // `count` MSMs of n points each, pipelined over pipeline_slots slots, each with its own stream and
@@ -1469,7 +1484,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       bs->p[m] = in.scalars[b];
       if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
         const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
-        bs->p[m] = sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
+        bs->p[m] = in.dev_scalars ? in.dev_scalars[j * nm + mr] : sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
         if (!shared) bp->p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
       }
     }
@@ -1501,7 +1516,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       }
       return true;
     };
-    if (!up(in.scalars, bs, 8)) return MSM_ERR_HIP;
+    if (!in.dev_scalars && !up(in.scalars, bs, 8)) return MSM_ERR_HIP;
     for (uint32_t m = 0; m < nreal && !shared; m++) {
       const size_t len = len_of(std::min(j * nm + m, count - 1));
       if (len < n) {
@@ -1675,8 +1690,16 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
 size_t host_tail() {
   static const size_t v = getenv("MSM_HOST_TAIL_LOG") ? (atoi(getenv("MSM_HOST_TAIL_LOG")) > 0
                                                             ? (size_t)1 << atoi(getenv("MSM_HOST_TAIL_LOG")) : 0)
-                                                      : (size_t)1 << 15;
+                                                      : 0;
   return v;
+}
+
+// Whether the split uploads all the scalars in one copy before the first launch's points
+// (MSM_HOST_SC_FIRST=0: per launch, beside its points): one copy instead of one per launch, so
+// fewer ~20-us gaps between copies, and every launch's sort can start as soon as it is enqueued.
+bool host_scalars_first() {
+  static const bool on = !(getenv("MSM_HOST_SC_FIRST") && atoi(getenv("MSM_HOST_SC_FIRST")) == 0);
+  return on;
 }
 
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
@@ -1707,9 +1730,20 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   in.scalars = ss.data();
   in.batch = nmb;
   in.lens = lens.data();
+  std::vector<const uint32_t*> dsc(G);
+  if (host_scalars_first() && t == 0) {
+    // one copy of all n scalars (+ s words of room: the last slice's device padding)
+    if (int rc = c->host_sc.ensure((n + s) * 32)) return rc;
+    HIPCHECK(hipMemcpyAsync(c->host_sc.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->copy_stream));
+    for (size_t g = 0; g < G; g++) dsc[g] = c->host_sc.as<uint32_t>() + (g * s) * 8;
+    in.dev_scalars = dsc.data();
+  }
   std::vector<Pt> part(G, pt_identity());
   int rc = run_many(c, in, s, G, o, nullptr, nullptr, true, part.data());
-  if (rc != MSM_OK) return rc;
+  if (rc != MSM_OK) {
+    hipStreamSynchronize(c->copy_stream);  // the scalar copy reads the caller's array
+    return rc;
+  }
   Pt acc = part[0];
   for (size_t g = 1; g < G; g++) acc = pt_add(acc, part[g]);
   *result = acc;
@@ -1768,13 +1802,17 @@ int device_list(const msm_opts* o, std::vector<int>* devs) {
   return MSM_OK;
 }
 
-// One listed device's single-device options.
+// One listed device's single-device options (a window range carried over).
 msm_opts opts_on(const msm_opts* o, int device) {
   msm_opts r{};
   r.window_bits = o->window_bits;
   r.run_length = o->run_length;
   r.flags = o->flags & ~MSM_FLAG_DEVICES;
   r.device = device;
+  if (o->flags & MSM_FLAG_WINDOWS) {
+    r.window_lo = o->window_lo;
+    r.window_hi = o->window_hi;
+  }
   return r;
 }
 
@@ -1967,6 +2005,7 @@ void msm_shutdown(void) {
     hipStreamSynchronize(c->copy_stream);
     for (Slot& sl : c->slot) hipStreamSynchronize(sl.stream);
     c->shared_pts.release();
+    c->host_sc.release();
     for (Slot& sl : c->slot) {
       sl.ws.release();
       for (Segment& sg : sl.seg) sg.drop();
@@ -2185,6 +2224,11 @@ int msm_point_add_affine(const uint32_t a_xy_be[16], const uint32_t b_xy_be[16],
   Pt r = pt_add(pt_from_affine_std(ax, ay), pt_from_affine_std(bx, by));
   pt_to_be_affine(r, out_xy_be);
   return MSM_OK;
+}
+
+uint32_t msm_window_count(uint32_t window_bits) {
+  if (window_bits < 4 || window_bits > 20) return 0;
+  return (MAIN_BITS + window_bits - 1) / window_bits + 1;  // balanced main windows + the overflow window
 }
 
 uint32_t msm_split_windows(uint32_t window_bits) {

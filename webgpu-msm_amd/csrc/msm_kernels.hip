@@ -315,14 +315,15 @@ constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
 constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup
 template <typename T>
 // blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its windows
-// [y Wm, (y+1) Wm).
+// [y Wr, (y+1) Wr).  Every window is recoded (the carries climb through them all); only the
+// launch's window range [d.w0, d.w0 + d.Wr) is written and counted.
 __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_sets, MsmDims d,
                                                             T* __restrict__ digits, uint32_t* __restrict__ colsum) {
-  extern __shared__ uint32_t lds_hist[];  // [Wm][nbc]
+  extern __shared__ uint32_t lds_hist[];  // [Wr][nbc]
   const uint32_t* __restrict__ scalars = scalar_sets.p[blockIdx.y];
   const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
-  const uint32_t w0 = blockIdx.y * d.Wm;
-  const uint32_t nh = d.Wm * d.nbc;
+  const uint32_t w0 = blockIdx.y * d.Wr;
+  const uint32_t nh = d.Wr * d.nbc;
   for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) lds_hist[b] = 0;
   __syncthreads();
   // (loading all of a lane's scalars before recoding any measured slower: 43 vs 37 us per
@@ -330,7 +331,9 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
   for (uint32_t i = lo + threadIdx.x; i < hi; i += RC_THREADS) {
     uint32_t s[8];
     load_scalar(scalars, i, s);
-    recode(s, d, [&](uint32_t w, int32_t digit) {
+    recode(s, d, [&](uint32_t wa, int32_t digit) {
+      const uint32_t w = wa - d.w0;  // local window (wraps to >= Wr below the range)
+      if (w >= d.Wr) return;
       uint32_t code = DigitCode<T>::ZERO;
       if (digit != 0) {
         const uint32_t mag = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
@@ -466,7 +469,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict
   uint32_t* lcnt = dyn;
   uint32_t* gstart = dyn + d.nbc;
   const uint32_t w = blockIdx.y, ck = blockIdx.x;
-  const uint32_t pbase = d.shared ? 0u : (w / d.Wm) * d.n;  // first point record of this window's MSM
+  const uint32_t pbase = d.shared ? 0u : (w / d.Wr) * d.n;  // first point record of this window's MSM
   const T* dw = digits + (size_t)w * d.n;
   const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
   uint32_t code[PS_R], rank[PS_R];
@@ -1108,46 +1111,49 @@ extern "C" __global__ void __launch_bounds__(LS_THREADS) k_lead_scan(uint32_t* _
 #endif
 constexpr uint32_t RED1_THREADS = MSM_RED1_THREADS;
 
-// Lane -> (window, chunk) of k_bucket_reduce_1.  Live chunks (those holding buckets a digit of
-// their window can reach) of every MSM's main windows come first, so real work is whole waves at
-// the front of the grid; then the empty ones: the upper halves of (q)-bit windows in a
-// (q+1)-bit table, and the overflow windows (empty for canonical scalars).
+// Chunks of a window that a digit can reach (its "live" chunks; the others hold no entry): a main
+// window of the table's full width fills every chunk, a (q)-bit window in a (q+1)-bit table its
+// lower half, and the overflow window (|digit| <= 4, buckets 0..3) is counted dead altogether (it
+// is empty for canonical scalars).  `a` is the window's index in its MSM.
+__host__ __device__ __forceinline__ uint32_t red1_live_chunks(const MsmDims& d, uint32_t L, uint32_t nchunks,
+                                                              uint32_t a) {
+  if (a + 1 == d.Wm) return 0;
+  if (d.nhi == 0 || a < d.nhi) return nchunks;
+  return (d.B / 2 + L - 1) / L;
+}
+
+// Lane -> (window, chunk) of k_bucket_reduce_1.  Live chunks of every MSM's windows come first, so
+// real work is whole waves at the front of the grid; then the dead ones (empty unless the scalars
+// are non-canonical), which exit early.
 __device__ __forceinline__ bool red1_lane(const MsmDims& d, uint32_t L, uint32_t nchunks, uint32_t gd, uint32_t& w,
                                           uint32_t& c) {
-  const uint32_t nmain = d.Wm - 1;
-  const uint32_t lc_hi = nchunks;                                // (c)-bit windows: every chunk live
-  const uint32_t nfull = d.nhi ? d.nhi : nmain;                  // windows of the table's full width
-  const uint32_t lc_lo = d.nhi ? (d.B / 2 + L - 1) / L : nchunks;  // (c-1)-bit windows
-  const uint32_t live = nfull * lc_hi + (nmain - nfull) * lc_lo;  // per MSM
+  uint32_t live = 0;  // per MSM
+  for (uint32_t l = 0; l < d.Wr; l++) live += red1_live_chunks(d, L, nchunks, d.w0 + l);
+  const uint32_t dead = d.Wr * nchunks - live;
+  uint32_t r, m;
+  bool in_live;
   if (gd < d.nm * live) {
-    const uint32_t m = gd / live, r = gd % live;
-    if (r < nfull * lc_hi) {
-      w = r / lc_hi;
-      c = r % lc_hi;
-    } else {
-      const uint32_t r2 = r - nfull * lc_hi;
-      w = nfull + r2 / lc_lo;
-      c = r2 % lc_lo;
-    }
-    w += m * d.Wm;
-    return true;
-  }
-  // dead region: per MSM, (nmain - nfull) windows x (nchunks - lc_lo) empty chunks, then the
-  // overflow window's nchunks chunks
-  const uint32_t dead_lo = (nmain - nfull) * (nchunks - lc_lo);
-  const uint32_t per = dead_lo + nchunks;
-  const uint32_t r0 = gd - d.nm * live;
-  if (r0 >= d.nm * per) return false;
-  const uint32_t m = r0 / per, r = r0 % per;
-  if (r < dead_lo) {
-    const uint32_t span = nchunks - lc_lo;
-    w = m * d.Wm + nfull + r / span;
-    c = lc_lo + r % span;
+    m = gd / live;
+    r = gd % live;
+    in_live = true;
   } else {
-    w = m * d.Wm + nmain;
-    c = r - dead_lo;
+    const uint32_t r0 = gd - d.nm * live;
+    if (r0 >= d.nm * dead) return false;
+    m = r0 / dead;
+    r = r0 % dead;
+    in_live = false;
   }
-  return true;
+  for (uint32_t l = 0; l < d.Wr; l++) {
+    const uint32_t lc = red1_live_chunks(d, L, nchunks, d.w0 + l);
+    const uint32_t span = in_live ? lc : nchunks - lc;
+    if (r < span) {
+      w = m * d.Wr + l;
+      c = in_live ? r : lc + r;
+      return true;
+    }
+    r -= span;
+  }
+  return false;
 }
 
 template <uint32_t RL>

@@ -24,7 +24,7 @@ __all__ = [
     "compute_msm_shared_device", "compute_msm_many", "compute_msm_shared", "compute_msm_cpu", "MSM_FLAG_SERIAL",
     "combine_partials", "combine_partials_many", "point_add_affine",
     "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count", "device_ordinals",
-    "MSM_FLAG_DEVICES", "MSM_MAX_DEVICES",
+    "MSM_FLAG_DEVICES", "MSM_FLAG_WINDOWS", "MSM_MAX_DEVICES", "window_count",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
 
@@ -44,11 +44,11 @@ class MsmError(RuntimeError):
 
 class MsmOpts(ctypes.Structure):
     """include/msm.h msm_opts: the original four fields, then the device list (read by libmsm only
-    when flags has MSM_FLAG_DEVICES)."""
+    when flags has MSM_FLAG_DEVICES), then the window range (MSM_FLAG_WINDOWS)."""
     _fields_ = [("window_bits", ctypes.c_uint32), ("run_length", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("devices", ctypes.POINTER(ctypes.c_int32)), ("n_devices", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("reserved", ctypes.c_uint32), ("window_lo", ctypes.c_uint32), ("window_hi", ctypes.c_uint32)]
 
 
 class MsmProfile(ctypes.Structure):
@@ -62,6 +62,7 @@ class MsmProfile(ctypes.Structure):
 
 MSM_FLAG_SERIAL = 1  # pipelined entries: one launch in flight at a time
 MSM_FLAG_DEVICES = 2  # msm_opts carries a device list (include/msm.h)
+MSM_FLAG_WINDOWS = 4  # msm_opts carries a window range
 MSM_MAX_DEVICES = 16
 MSM_STREAM_NULL = 1  # hip_stream value: order after the null (legacy default) stream
 
@@ -119,6 +120,7 @@ def load() -> ctypes.CDLL:
         "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
         "msm_split": ([ctypes.c_uint32, vp, sz, u32p], ctypes.c_int),
         "msm_split_windows": ([ctypes.c_uint32], ctypes.c_uint32),
+        "msm_window_count": ([ctypes.c_uint32], ctypes.c_uint32),
         "msm_set_profiling": ([ctypes.c_int], ctypes.c_int),
         "msm_gen_points": ([u32p, ctypes.c_uint64, ctypes.c_uint64, sz, u32p], ctypes.c_int),
         "msm_gen_scalars": ([ctypes.c_uint64, sz, u32p], ctypes.c_int),
@@ -169,10 +171,15 @@ def _out(n: int) -> Tuple[np.ndarray, ctypes.POINTER(ctypes.c_uint32)]:
 
 
 def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: int = -1, flags: int = 0,
-          devices: Optional[Sequence[int]] = None):
+          devices: Optional[Sequence[int]] = None, windows: Optional[Tuple[int, int]] = None):
     """A msm_opts by reference.  `devices` (a list of HIP ordinals) runs the call on several
-    devices (MSM_FLAG_DEVICES); the array is kept alive by the returned object."""
+    devices (MSM_FLAG_DEVICES); the array is kept alive by the returned object.  `windows` =
+    (lo, hi) restricts the MSM to those signed-digit windows (MSM_FLAG_WINDOWS; needs an explicit
+    window_size)."""
     o = MsmOpts(int(window_size or 0), int(run_length or 0), int(device), int(flags))
+    if windows is not None:
+        o.window_lo, o.window_hi = int(windows[0]), int(windows[1])
+        o.flags |= MSM_FLAG_WINDOWS
     if devices is not None:
         arr = (ctypes.c_int32 * max(len(devices), 1))(*[int(d) for d in devices])
         o.devices = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
@@ -271,16 +278,24 @@ def compute_msm(base_affine_points, scalars, window_size: Optional[int] = None,
 
 
 def compute_msm_partial(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
-                        device: int = -1, devices: Optional[Sequence[int]] = None) -> np.ndarray:
+                        device: int = -1, devices: Optional[Sequence[int]] = None,
+                        windows: Optional[Tuple[int, int]] = None) -> np.ndarray:
     L = load()
     pts = _u32(points_wire).reshape(-1, 32)
     sc = _u32(scalars_wire).reshape(-1, 8)
     n = min(pts.shape[0], sc.shape[0])
     pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
     o, op = _out(32)
-    _check(L.msm_compute_partial(_ptr(pts), _ptr(sc), n, _opts(window_size, None, device, devices=devices), op),
+    _check(L.msm_compute_partial(_ptr(pts), _ptr(sc), n,
+                                 _opts(window_size, None, device, devices=devices, windows=windows), op),
            "msm_compute_partial")
     return o
+
+
+def window_count(window_size: int) -> int:
+    """Signed-digit windows of an MSM at window width c, overflow window included
+    (msm_window_count): the index space of the `windows=(lo, hi)` ranges."""
+    return int(load().msm_window_count(int(window_size)))
 
 
 def _dev_ptr(t) -> int:
@@ -321,11 +336,12 @@ def compute_msm_device(d_points, d_scalars, n: int, window_size: Optional[int] =
 
 def compute_msm_device_partial(d_points, d_scalars, n: int, window_size: Optional[int] = None,
                                device: int = -1, stream: int = 0,
-                               devices: Optional[Sequence[int]] = None) -> np.ndarray:
+                               devices: Optional[Sequence[int]] = None,
+                               windows: Optional[Tuple[int, int]] = None) -> np.ndarray:
     L = load()
     o, op = _out(32)
     _check(L.msm_compute_device_partial(_dev_ptr(d_points), _dev_ptr(d_scalars), n,
-                                        _opts(window_size, None, device, devices=devices),
+                                        _opts(window_size, None, device, devices=devices, windows=windows),
                                         _stream(stream, d_points, d_scalars), op), "msm_compute_device_partial")
     return o
 
@@ -436,7 +452,8 @@ def compute_msm_cpu(points_wire, scalars_wire, window_size: Optional[int] = None
 
 def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_size: Optional[int] = None,
                                     run_length: Optional[int] = None, device: int = -1,
-                                    stream: int = 0, flags: int = 0) -> np.ndarray:
+                                    stream: int = 0, flags: int = 0,
+                                    windows: Optional[Tuple[int, int]] = None) -> np.ndarray:
     """compute_msm_many_device, each result as a projective X|Y|T|Z partial: [count][32] BE words."""
     L = load()
     count = len(points_list)
@@ -446,7 +463,7 @@ def compute_msm_many_device_partial(points_list, scalars_list, n: int, window_si
     ss = (ctypes.c_void_p * max(count, 1))(*[_dev_ptr(t) for t in scalars_list])
     o, op = _out(32 * max(count, 1))
     _check(L.msm_compute_many_device_partial(ctypes.cast(pp, ctypes.c_void_p), ctypes.cast(ss, ctypes.c_void_p), n,
-                                             count, _opts(window_size, run_length, device, flags),
+                                             count, _opts(window_size, run_length, device, flags, windows=windows),
                                              _stream(stream, _first(points_list), _first(scalars_list)), op),
            "msm_compute_many_device_partial")
     return o[:32 * count].reshape(count, 32)

@@ -1,11 +1,14 @@
-"""Point-sharded multi-GPU MSM: one process per GPU, partial points joined over RCCL/xGMI.
+"""Sharded multi-GPU MSM: one process per GPU, partial points joined over RCCL/xGMI.
 
 MSM is linear in the (point, scalar) vector, so every rank computes the MSM of a contiguous
 1/world slice of the inputs on its own GPU (no data-path collective) and the per-rank partial
 points (projective X|Y|T|Z, 128 B each) are all-gathered and added on rank 0 — the
 generalisation of the reference's CPU/GPU co-compute split and its single affine join
 (src/submission/submission.ts:116-154, msm-wasm/src/lib.rs:240-253).  The join is an elliptic
-curve addition, not an RCCL reduction op, hence all_gather + host add.
+curve addition, not an RCCL reduction op, hence all_gather + host add.  The MSM is also a sum
+over its signed-digit windows, so a points x windows split (P point shards times Q window ranges,
+P Q = world: split_part) joins the same way and gives each GPU fewer buckets per entry
+(DESIGN.md §6).
 """
 from __future__ import annotations
 
@@ -17,6 +20,44 @@ import numpy as np
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous [lo, hi) slice of n points owned by `rank` (sizes differ by at most 1)."""
     return n * rank // world, n * (rank + 1) // world
+
+
+SPLIT_WINDOW_BITS = 16  # window width of a windows split (every GPU must cut the same windows)
+
+
+def window_ranges(wm: int, q: int):
+    """q contiguous ranges of an MSM's wm signed-digit windows: the wm - 1 main windows balanced,
+    the overflow window (empty for canonical scalars) with the top range."""
+    main = wm - 1
+    edges = [round(main * i / q) for i in range(q + 1)]
+    edges[-1] = wm
+    return list(zip(edges[:-1], edges[1:]))
+
+
+def parse_split(split: str, world: int) -> Tuple[int, int]:
+    """"PxQ" -> (P, Q) with P * Q == world: P point shards times Q window ranges.
+    "points" is world x 1 (every GPU a 1/world of the points, all windows)."""
+    if split in ("", "points", "auto"):
+        return world, 1
+    p, q = (int(v) for v in split.lower().split("x"))
+    if p < 1 or q < 1 or p * q != world:
+        raise ValueError(f"split {split!r} does not factor {world} GPUs as points x windows")
+    return p, q
+
+
+def split_part(n: int, rank: int, world: int, split: str = "points"):
+    """What GPU `rank` computes of an n-point MSM under a points x windows split: its point shard
+    [lo, hi), its window range (None: all windows) and the window width the range refers to (None:
+    the library's own choice).  Rank r takes point shard r // Q and window range r % Q; the partials
+    of all ranks sum to the MSM."""
+    from . import window_count
+
+    P, Q = parse_split(split, world)
+    lo, hi = shard_range(n, rank // Q, P)
+    if Q == 1:
+        return lo, hi, None, None
+    c = SPLIT_WINDOW_BITS
+    return lo, hi, window_ranges(window_count(c), Q)[rank % Q], c
 
 
 def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.ndarray:
@@ -54,22 +95,24 @@ def combine_on_root(parts: np.ndarray, rank: int, root: int = 0) -> Optional[Tup
 
 
 def sharded_msm_device(d_points, d_scalars, n_local: int, rank: int, device=None, window_size=None,
-                       group=None) -> Optional[Tuple[int, int]]:
+                       group=None, windows=None) -> Optional[Tuple[int, int]]:
     """One sharded MSM step: local partial on this rank's GPU, gather, join on rank 0."""
     from . import compute_msm_device_partial
 
-    part = compute_msm_device_partial(d_points, d_scalars, n_local, window_size=window_size)
+    part = compute_msm_device_partial(d_points, d_scalars, n_local, window_size=window_size, windows=windows)
     parts = gather_partials(part, device=device, group=group)
     return combine_on_root(parts, rank)
 
 
 def sharded_msm_many_device(points_list, scalars_list, n_local: int, rank: int, device=None, window_size=None,
-                            group=None):
+                            group=None, windows=None):
     """K sharded MSMs, pipelined: each rank computes its K partials through libmsm's pipelined
-    entry (msm_compute_many_device_partial), then ONE all_gather ships all K x 128 B and rank 0
-    joins them — the exchange is batched across the K independent MSMs."""
+    entry (msm_compute_many_device_partial; `windows` = its window range under a points x windows
+    split), then ONE all_gather ships all K x 128 B and rank 0 joins them — the exchange is batched
+    across the K independent MSMs."""
     from . import compute_msm_many_device_partial
 
-    parts = compute_msm_many_device_partial(points_list, scalars_list, n_local, window_size=window_size)
+    parts = compute_msm_many_device_partial(points_list, scalars_list, n_local, window_size=window_size,
+                                            windows=windows)
     gathered = gather_partials(parts, device=device, group=group)
     return combine_batch_on_root(gathered, rank)
