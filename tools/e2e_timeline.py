@@ -3,8 +3,9 @@
 
     python tools/e2e_timeline.py gpurun_out/<tag>_e2etrace_d [--call 3]
 
-Calls are separated by host->device gaps > 1 ms.  Per call: every copy and kernel (start, end,
-duration, relative to the call's first copy), the upload span, and what runs after the last copy.
+Calls are separated by device-idle gaps (no copy or kernel running) > --gap us.  Per call: every copy
+and kernel (start, end, duration, relative to the call's first copy), the upload span, the gaps
+between consecutive copies, and what runs after the last copy.
 """
 import argparse
 import csv
@@ -13,6 +14,7 @@ import os
 ap = argparse.ArgumentParser()
 ap.add_argument("d")
 ap.add_argument("--call", type=int, default=-2, help="which call (python index) to print in full")
+ap.add_argument("--gap", type=float, default=150.0, help="device-idle gap (us) that separates calls")
 a = ap.parse_args()
 cp = list(csv.DictReader(open(os.path.join(a.d, "run_memory_copy_trace.csv"))))
 kn = list(csv.DictReader(open(os.path.join(a.d, "run_kernel_trace.csv"))))
@@ -23,7 +25,7 @@ ev += [(r["Kernel_Name"].replace("void msm::", "").split("(")[0].split("<")[0][:
 ev.sort(key=lambda e: e[1])
 calls, cur, last = [], [], None
 for e in ev:
-    if last is not None and e[1] - last > 1_000_000:
+    if last is not None and e[1] - last > a.gap * 1e3:
         calls.append(cur)
         cur = []
     cur.append(e)
@@ -39,8 +41,11 @@ for ci, c in enumerate(calls):
     up = max(e[2] for e in copies)
     kbusy = sum(e[2] - e[1] for e in c if not e[0].startswith("copy"))
     cbusy = sum(e[2] - e[1] for e in copies)
-    print(f"call {ci}: span {(end - t0) / 1e3:8.1f} us, copies {len(copies)} busy {cbusy / 1e3:8.1f} us, "
-          f"upload ends {(up - t0) / 1e3:8.1f} us, after upload {(end - up) / 1e3:7.1f} us, kernels busy {kbusy / 1e3:8.1f}")
+    cs = sorted(copies, key=lambda e: e[1])
+    gaps = [(cs[i + 1][1] - cs[i][2]) / 1e3 for i in range(len(cs) - 1)]
+    print(f"call {ci}: span {(end - t0) / 1e3:8.1f} us, copies {len(copies)} busy {cbusy / 1e3:8.1f} us "
+          f"(gaps {sum(gaps):6.1f} us: {' '.join(f'{g:.0f}' for g in gaps)}), upload ends {(up - t0) / 1e3:8.1f} us, "
+          f"after upload {(end - up) / 1e3:7.1f} us, kernels busy {kbusy / 1e3:8.1f}")
 c = calls[a.call]
 t0 = c[0][1]
 for name, s, e, q in c:

@@ -115,6 +115,9 @@ for step in "$@"; do
         --no-extras "${BENCH_Q[@]}" ;;
     multidev) run multidev 300 python bench.py --multi-device --no-extras "${BENCH_Q[@]}" ;;
     split) run split 600 python tools/split_probe.py --gpus 8 ;;
+    split:*)  # split:D:SPLITS:C -- tools/split_probe.py over D GPUs for the listed PxQ splits at window width C
+      IFS=: read -r _ ng sp cw <<< "$step"
+      run "split${ng}_${sp//,/_}_c${cw}" 600 python tools/split_probe.py --gpus "$ng" --splits "$sp" --window "$cw" ;;
     kstats)
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;

@@ -644,7 +644,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
                        w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
                        w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total, joins ? 1u : 0u,
-                       reinterpret_cast<uint32_t*>(sl.h_out_dev));
+                       w.bucket_start.as<uint32_t>(), d.B, reinterpret_cast<uint32_t*>(sl.h_out_dev));
     mark(PH_RED2);
     mark(PH_READBACK);
   }
@@ -1684,16 +1684,6 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
 // overlaps all the compute but the last launch's; the partials are joined with G - 1 adds.  When
 // G does not divide n the last slice is short: it is padded on the device (identity points, zero
 // scalars) rather than run as a separate remainder MSM after the others.
-// Points per slice of the split's last launch (MSM_HOST_TAIL_LOG; 0 = no short tail slices): what
-// is left to compute once the last upload has landed is that launch's preparation, accumulation
-// and reduction, so the last launch is made short.
-size_t host_tail() {
-  static const size_t v = getenv("MSM_HOST_TAIL_LOG") ? (atoi(getenv("MSM_HOST_TAIL_LOG")) > 0
-                                                            ? (size_t)1 << atoi(getenv("MSM_HOST_TAIL_LOG")) : 0)
-                                                      : 0;
-  return v;
-}
-
 // Whether the split uploads all the scalars in one copy before the first launch's points
 // (MSM_HOST_SC_FIRST=0: per launch, beside its points): one copy instead of one per launch, so
 // fewer ~20-us gaps between copies, and every launch's sort can start as soon as it is enqueued.
@@ -1704,25 +1694,25 @@ bool host_scalars_first() {
 
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
-  // The body: Gb slices (a whole number of launches) of at most s points, balanced; then one
-  // launch of short tail slices of t points each.  Every slice is an MSM of s points to the
-  // pipelined entry (in.lens: a short slice is padded on the device with identity points and zero
-  // scalars, which add no bucket entries).
+  // G <= 16 balanced slices of s points, a whole number of launches of nmb slices (every slice
+  // is an MSM of s points to the pipelined entry; in.lens: a short slice is padded on the device
+  // with identity points and zero scalars, which add no bucket entries).  (Short tail slices for
+  // the last launch -- its compute is what is left after the last upload -- measured slower: one
+  // more launch costs more than the shorter tail saves)
   const uint32_t nmb = host_batch();
-  size_t t = host_tail();
-  if (t * nmb * 8 > n) t = 0;  // small MSMs: no tail launch
-  const size_t body = n - t * nmb;
-  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, body / host_piece()));
+  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, n / host_piece()));
   Gb = (Gb + nmb - 1) / nmb * nmb;
-  const size_t s = (body + Gb - 1) / Gb;
-  const size_t G = Gb + (t ? nmb : 0);
+  const size_t s = (n + Gb - 1) / Gb;
+  std::vector<size_t> offs, lens;
+  for (size_t g = 0; g < Gb; g++) {
+    offs.push_back(std::min(g * s, n));
+    lens.push_back(g * s < n ? std::min(s, n - g * s) : 0);  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
+  }
+  const size_t G = offs.size();
   std::vector<const uint32_t*> pp(G), ss(G);
-  std::vector<size_t> lens(G);
   for (size_t g = 0; g < G; g++) {
-    const size_t off = g < Gb ? g * s : body + (g - Gb) * t;
-    pp[g] = points_be + off * 32;
-    ss[g] = scalars_be + off * 8;
-    lens[g] = g < Gb ? (g * s < body ? std::min(s, body - g * s) : 0) : t;  // 0 only for tiny overrides
+    pp[g] = points_be + offs[g] * 32;
+    ss[g] = scalars_be + offs[g] * 8;
   }
   ManyInputs in;
   in.kind = ManyInputs::HOST;
@@ -1731,11 +1721,25 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   in.batch = nmb;
   in.lens = lens.data();
   std::vector<const uint32_t*> dsc(G);
-  if (host_scalars_first() && t == 0) {
-    // one copy of all n scalars (+ s words of room: the last slice's device padding)
-    if (int rc = c->host_sc.ensure((n + s) * 32)) return rc;
-    HIPCHECK(hipMemcpyAsync(c->host_sc.p, scalars_be, n * 32, hipMemcpyHostToDevice, c->copy_stream));
-    for (size_t g = 0; g < G; g++) dsc[g] = c->host_sc.as<uint32_t>() + (g * s) * 8;
+  if (host_scalars_first()) {
+    // slice g's scalars at g s in one device buffer (s words each, the tail of a short slice is
+    // its device padding): the run of full slices at the front goes up in one copy, every other
+    // slice in its own
+    if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
+    uint32_t* base = c->host_sc.as<uint32_t>();
+    for (size_t g = 0; g < G;) {
+      size_t h = g + 1;
+      if (lens[g] == s)
+        while (h < G && lens[h] == s && offs[h] == offs[g] + (h - g) * s) h++;
+      const size_t words = (h - g == 1 ? lens[g] : (h - g) * s) * 8;
+      if (words && hipMemcpyAsync(base + g * s * 8, scalars_be + offs[g] * 8, words * 4, hipMemcpyHostToDevice,
+                                  c->copy_stream) != hipSuccess) {
+        hipStreamSynchronize(c->copy_stream);
+        return MSM_ERR_HIP;
+      }
+      g = h;
+    }
+    for (size_t g = 0; g < G; g++) dsc[g] = base + g * s * 8;
     in.dev_scalars = dsc.data();
   }
   std::vector<Pt> part(G, pt_identity());

@@ -1240,48 +1240,58 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
                                                                              uint32_t* __restrict__ skew_list,
                                                                              const uint32_t* __restrict__ total,
                                                                              uint32_t final_pass,
+                                                                             const uint32_t* __restrict__ bucket_start,
+                                                                             uint32_t B,
                                                                              uint32_t* __restrict__ out_host) {
   __shared__ uint32_t sh[RED2_THREADS / 2][PT_WORDS];
   const uint32_t w = blockIdx.x / nterms, term = blockIdx.x % nterms;
-  const bool vterm = term < nv;
-  const uint32_t* src = vterm ? in_U : in_T;
-  const uint32_t kbit = term - nv;
-  // A V slice is ceil(nchunks/nv) consecutive chunks; a bit term enumerates its j-th chunk with
-  // bit k set directly (j < pow2ceil(nchunks)/2, chunks past the end skipped), so every lane
-  // loads about the same number of points (a stride-and-skip loop over all chunks would give half
-  // the lanes all the work for k < 10).
-  const uint32_t vslice = (nchunks + nv - 1) / nv;
-  uint32_t half_n = 1;
-  while (2 * half_n < nchunks) half_n <<= 1;
-  xyzt acc = pt_identity();
-  bool live = false;
-  for (uint32_t j = threadIdx.x; j < (vterm ? vslice : half_n); j += RED2_THREADS) {
-    const uint32_t c = vterm ? term * vslice + j : (((j >> kbit) << (kbit + 1)) | (1u << kbit) | (j & ((1u << kbit) - 1u)));
-    if (c >= nchunks) continue;
-    xyzt p = load_pt(src + ((size_t)w * nchunks + c) * PT_WORDS);
-    acc = live ? pt_add(acc, p) : p;
-    live = true;
-  }
-  // tree reduce through LDS: upper half hands its point to the lower half each round.  The wide
-  // levels add one point per lane; from RED2_QUAD points down, each add is spread over a quad of
-  // lanes (pt_add_quad: 3 multiply latencies instead of 9) since those levels are latency-bound.
-  for (uint32_t half = RED2_THREADS / 2; half >= RED2_QUAD; half >>= 1) {
-    if (threadIdx.x >= half && threadIdx.x < 2 * half) store_pt_lds(sh[threadIdx.x - half], acc);
+  // a window without entries (the overflow window of canonical scalars, a window range's empty
+  // windows) has identity terms: skip its loads and latency-bound tree
+  const bool empty = bucket_start[(size_t)w * B] == bucket_start[(size_t)(w + 1) * B];
+  if (empty) {
+    if (threadIdx.x == 0) store_pt_lds(sh[0], pt_identity());
     __syncthreads();
-    if (threadIdx.x < half) acc = pt_add(acc, load_pt_lds(sh[threadIdx.x]));
+  } else {
+    const bool vterm = term < nv;
+    const uint32_t* src = vterm ? in_U : in_T;
+    const uint32_t kbit = term - nv;
+    // A V slice is ceil(nchunks/nv) consecutive chunks; a bit term enumerates its j-th chunk with
+    // bit k set directly (j < pow2ceil(nchunks)/2, chunks past the end skipped), so every lane
+    // loads about the same number of points (a stride-and-skip loop over all chunks would give half
+    // the lanes all the work for k < 10).
+    const uint32_t vslice = (nchunks + nv - 1) / nv;
+    uint32_t half_n = 1;
+    while (2 * half_n < nchunks) half_n <<= 1;
+    xyzt acc = pt_identity();
+    bool live = false;
+    for (uint32_t j = threadIdx.x; j < (vterm ? vslice : half_n); j += RED2_THREADS) {
+      const uint32_t c = vterm ? term * vslice + j : (((j >> kbit) << (kbit + 1)) | (1u << kbit) | (j & ((1u << kbit) - 1u)));
+      if (c >= nchunks) continue;
+      xyzt p = load_pt(src + ((size_t)w * nchunks + c) * PT_WORDS);
+      acc = live ? pt_add(acc, p) : p;
+      live = true;
+    }
+    // tree reduce through LDS: upper half hands its point to the lower half each round.  The wide
+    // levels add one point per lane; from RED2_QUAD points down, each add is spread over a quad of
+    // lanes (pt_add_quad: 3 multiply latencies instead of 9) since those levels are latency-bound.
+    for (uint32_t half = RED2_THREADS / 2; half >= RED2_QUAD; half >>= 1) {
+      if (threadIdx.x >= half && threadIdx.x < 2 * half) store_pt_lds(sh[threadIdx.x - half], acc);
+      __syncthreads();
+      if (threadIdx.x < half) acc = pt_add(acc, load_pt_lds(sh[threadIdx.x]));
+      __syncthreads();
+    }
+    if (threadIdx.x < RED2_QUAD) store_pt_lds(sh[threadIdx.x], acc);
     __syncthreads();
-  }
-  if (threadIdx.x < RED2_QUAD) store_pt_lds(sh[threadIdx.x], acc);
-  __syncthreads();
-  {
-    const uint32_t j = threadIdx.x >> 2, q = threadIdx.x & 3;
-    for (uint32_t half = RED2_QUAD / 2; half >= 1; half >>= 1) {
-      const bool act = j < half;  // uniform across a quad
-      fe res;
-      if (act) res = pt_add_quad(load_fe_lds(&sh[j][q * NL]), load_fe_lds(&sh[j + half][q * NL]));
-      __syncthreads();
-      if (act) store_fe_lds(&sh[j][q * NL], res);
-      __syncthreads();
+    {
+      const uint32_t j = threadIdx.x >> 2, q = threadIdx.x & 3;
+      for (uint32_t half = RED2_QUAD / 2; half >= 1; half >>= 1) {
+        const bool act = j < half;  // uniform across a quad
+        fe res;
+        if (act) res = pt_add_quad(load_fe_lds(&sh[j][q * NL]), load_fe_lds(&sh[j + half][q * NL]));
+        __syncthreads();
+        if (act) store_fe_lds(&sh[j][q * NL], res);
+        __syncthreads();
+      }
     }
   }
   if (threadIdx.x < 4) {  // one lane per coordinate (X, Y, T, Z): the conversions run side by side

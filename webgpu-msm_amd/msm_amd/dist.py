@@ -22,7 +22,10 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
-SPLIT_WINDOW_BITS = 16  # window width of a windows split (every GPU must cut the same windows)
+# Window width of a windows split (every GPU must cut the same windows): c = 15 measured best for
+# 2^20 points as 4 point shards x 2 window ranges over 8 GPUs (slowest GPU 0.203 ms per MSM against
+# 0.212 at c = 16 and 0.226 at c = 14; profiles/r4/split_probe.jsonl).
+SPLIT_WINDOW_BITS = 15
 
 
 def window_ranges(wm: int, q: int):
