@@ -20,6 +20,7 @@
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
 #   split        per-GPU work of every points x windows split of a 2^20 MSM over 8 GPUs, on this one
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
+#   ktrace:VAR=A,B  kernel trace of the pipelined bench per value of one knob (tools/pipeline_timeline.py)
 #   kstats1      the same on one stream, kernels in order (MSM_SLOTS=1 MSM_FORK_PREP=0), two-MSM 2^20
 #                launches only (the serial pass warms the GPU first, so the trace averages the
 #                launches kernel_ms measures)
@@ -121,6 +122,15 @@ for step in "$@"; do
     kstats)
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;
+    ktrace:*)  # ktrace:VAR=A,B -- rocprofv3 kernel trace of the pipelined bench for each value of one knob
+      IFS=: read -r _ spec <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for v in ${vals//,/ }; do
+        export "$var=$v"
+        run "ktrace_${var}_$v" 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "gpurun_out/${TAG}_ktrace_${var}_${v}_d" -o run -- python3 bench.py --no-extras "${BENCH_Q[@]}" --steps 40 --warmup 10
+        unset "$var"
+      done ;;
     kstats1)
       # shellcheck disable=SC2086
       MSM_SLOTS=1 MSM_FORK_PREP=0 run "kstats1${KS:-}" 300 rocprofv3 --kernel-trace --stats --output-format csv \

@@ -207,7 +207,6 @@ struct Slot {
   hipEvent_t ev_start = nullptr, ev_acc0 = nullptr, ev_acc1 = nullptr, ev_end = nullptr, ev_done = nullptr;
   hipEvent_t ev_in = nullptr;  // inputs of the slot's next launch are in place (uploads, caller's stream)
   hipEvent_t ev_sc = nullptr;  // the scalars of the slot's next launch are in place (host uploads)
-  hipEvent_t ev_accd = nullptr;  // the slot's last k_accumulate is done (staggered launches)
   Plan pl{};
   bool acc_timed = false;
 };
@@ -309,7 +308,6 @@ int get_ctx(int device, DevCtx** out) {
       hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_sc, hipEventDisableTiming);
-      hipEventCreateWithFlags(&sl.ev_accd, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_fork, hipEventDisableTiming);
       hipEventCreateWithFlags(&sl.ev_join, hipEventDisableTiming);
     }
@@ -1388,14 +1386,6 @@ bool host_sort_early() {
   return on;
 }
 
-// Whether pipelined launches are staggered: launch j's preparation and sort wait for launch j-1's
-// accumulation to finish, so they run beside j-1's bucket reduction (one wave per SIMD, no LDS)
-// instead of beside an accumulation that holds every CU (MSM_STAGGER=0/1 for A/B runs).
-bool stagger_launches() {
-  static const bool on = getenv("MSM_STAGGER") && atoi(getenv("MSM_STAGGER")) == 1;
-  return on;
-}
-
 // Where the inputs of one pipelined run come from.
 struct ManyInputs {
   enum Kind { DEVICE, HOST } kind = DEVICE;
@@ -1598,7 +1588,6 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // runs after j is enqueued, so the device holds nslot launches while the host works
   // (otherwise launches that finish together leave the device idle for a Horner each).
   std::vector<uint32_t> terms;
-  const bool stagger = nslot > 1 && !host && c->profiling == 0 && stagger_launches();
   for (size_t j = 0; j < nbatch + nslot; j++) {
     const bool have = j >= (size_t)nslot;
     const size_t f = have ? j - nslot : 0;
@@ -1625,17 +1614,8 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         if (hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess) return fail(MSM_ERR_HIP);
       }
       sl.pl = pl;
-      const int lp = sort_early ? parts & ~PART_SORT : parts;
-      if (stagger) {
-        // launch j's sort and preparation after launch j-1's accumulation; its reduction after its own
-        if (j > 0 && hipStreamWaitEvent(sl.stream, c->slot[(j - 1) % nslot].ev_accd, 0) != hipSuccess)
-          return fail(MSM_ERR_HIP);
-        if ((rc = launch_parts(c, pl, bp, bs, si, lp & ~PART_POST, pts)) != MSM_OK) return fail(rc);
-        if (hipEventRecord(sl.ev_accd, sl.stream) != hipSuccess) return fail(MSM_ERR_HIP);
-        if ((rc = launch_parts(c, pl, bp, bs, si, lp & PART_POST, pts)) != MSM_OK) return fail(rc);
-      } else if ((rc = launch_parts(c, pl, bp, bs, si, lp, pts)) != MSM_OK) {
+      if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
         return fail(rc);
-      }
       enqueued.store(j + 1, std::memory_order_release);
     }
     if (have) {
@@ -2036,7 +2016,7 @@ void msm_shutdown(void) {
       sl.h_out.release();
       sl.h_out_dev = nullptr;
       for (hipEvent_t e : {sl.ev_start, sl.ev_acc0, sl.ev_acc1, sl.ev_end, sl.ev_done, sl.ev_in, sl.ev_sc, sl.ev_fork,
-                          sl.ev_join, sl.ev_accd})
+                          sl.ev_join})
         if (e) hipEventDestroy(e);
     }
     for (int i = 0; i < PH_COUNT; i++) hipEventDestroy(c->ev[i]);
