@@ -6,8 +6,6 @@ survey pinned to the Aleo-wasm oracle at 2^12..2^20 (tests/golden/msm_vectors.js
 are bit-exact.
 """
 import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -73,34 +71,6 @@ def test_host_split_projective_points():
     assert e.value.code == -4
     # affine again: the same result
     assert M.compute_msm_wire(M.gen_points(n, k0=9, step=7), sc) == exp
-
-
-GRADED_CHILD = r"""
-import os, sys
-root = sys.argv[1]
-sys.path[:0] = [root, os.path.join(root, "webgpu-msm_amd"), os.path.join(root, "tests")]
-import msm_amd as M
-from _closed_form import closed_form
-for n, k0, step in ((1 << 20, 1, 1), ((1 << 19) + 7, 3, 5), (3 * (1 << 17) + 2, 2, 3)):
-    pts = M.gen_points(n, k0=k0, step=step)
-    sc = M.gen_scalars(n, seed=1000 + n % 97)
-    assert M.compute_msm_wire(pts, sc) == closed_form(k0, step, sc), n
-    assert M.compute_msm_wire(pts, sc) == closed_form(k0, step, sc), n  # replayed graphs
-print("ok")
-"""
-
-
-@pytest.mark.parametrize("tail", ["0", "17,16,16", "16,16", "17,16,15,15"])
-def test_host_split_graded_tail(tail):
-    # MSM_HOST_TAIL (read once per process, so each setting runs in a child): the last slices of a
-    # split host-input MSM run one per launch on plans of their own size after the body's
-    # two-slice launches; a tail that would leave fewer than two body slices is dropped (the
-    # 3 * 2^17 + 2 case for the longer tails)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MSM_HOST_TAIL=tail)
-    r = subprocess.run([sys.executable, "-c", GRADED_CHILD, root], capture_output=True, text=True, timeout=240,
-                       env=env)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
 
 
 def test_host_many_distinct():

@@ -1397,19 +1397,6 @@ struct ManyInputs {
                                  // the device with identity points and zero scalars); null: all n
   const uint32_t* const* dev_scalars = nullptr;  // host inputs whose scalars are already on the
                                                  // device (n + padding words per MSM): no scalar upload
-  // Graded tail (host inputs, not shared): the last tail_count MSMs run one per launch with
-  // tail_n[k] points each and their own plan, after the launches of the others (n points each).
-  const size_t* tail_n = nullptr;
-  size_t tail_count = 0;
-};
-
-// One launch of a pipelined run: MSMs [first, first + nreal) of the call, on a plan for nm MSMs of
-// n points each (a short last launch repeats its last MSM as padding).
-struct LaunchSpec {
-  size_t first = 0;
-  uint32_t nreal = 0;
-  size_t n = 0;
-  Plan pl{};
 };
 
 // `count` MSMs of n points each, pipelined over pipeline_slots slots, each with its own stream and
@@ -1439,43 +1426,23 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   const bool host = in.kind == ManyInputs::HOST;
   for (size_t b = 0; b < count; b++)
     if ((!shared && !in.points[b]) || !in.scalars[b]) return MSM_ERR_INVALID_ARG;
-  const size_t ntail = in.tail_n ? std::min(in.tail_count, count) : 0;
-  if (ntail && (shared || !host)) return MSM_ERR_INVALID_ARG;
-  const size_t body = count - ntail;
   // the batch's BatchPtrs hold MSM_MAX_BATCH entries: never more MSMs per launch than that
   const uint32_t nm = (uint32_t)std::min<size_t>(
-      in.batch ? std::min<size_t>(in.batch, std::max<size_t>(body, 1)) : pipeline_batch(n, std::max<size_t>(body, 1)),
-      MSM_MAX_BATCH);
-  std::vector<LaunchSpec> ls;
-  int rc = MSM_OK;
-  if (body) {
-    Plan pl;
-    if ((rc = make_plan(n, o, c->shape, &pl, count > 1, nm, shared)) != MSM_OK) return rc;
-    for (size_t f = 0; f < body; f += nm) ls.push_back({f, (uint32_t)std::min<size_t>(nm, body - f), n, pl});
-  }
-  for (size_t k = 0; k < ntail; k++) {
-    LaunchSpec t;
-    t.first = body + k;
-    t.nreal = 1;
-    t.n = in.tail_n[k];
-    if (t.n == 0 || t.n > n) return MSM_ERR_INVALID_ARG;
-    if ((rc = make_plan(t.n, o, c->shape, &t.pl, true, 1, false)) != MSM_OK) return rc;
-    ls.push_back(t);
-  }
-  const size_t nbatch = ls.size();
+      in.batch ? std::min<size_t>(in.batch, count) : pipeline_batch(n, count), MSM_MAX_BATCH);
+  const size_t nbatch = (count + nm - 1) / nm;
+  Plan pl;
+  int rc = make_plan(n, o, c->shape, &pl, count > 1, nm, shared);
+  if (rc != MSM_OK) return rc;
   // host inputs: one more launch in flight, so its upload queues behind the running ones
   // (2^20 msm_compute 4.21 -> 4.05 ms with three, profiles/r2t_*; device inputs are best with two)
   const int want = pipeline_slots(n, o) + (host && !(o && (o->flags & MSM_FLAG_SERIAL)) && !getenv("MSM_SLOTS") ? 1 : 0);
   const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)std::min(want, NSLOT)) : 1;
-  for (size_t j = 0; j < nbatch; j++) {  // every plan a slot will run, the largest first
-    const int si = (int)(j % nslot);
-    const LaunchSpec& L = ls[j];
-    if ((rc = ensure_workspace(c, L.pl, si)) != MSM_OK) return rc;
+  for (int si = 0; si < nslot; si++) {
+    if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
     if (host) {
       Workspace& w = c->slot[si].ws;
-      const size_t lm = L.pl.d.nm;
-      if ((!shared && (rc = w.wire_pts.ensure(lm * L.n * 128)) != MSM_OK) ||
-          (rc = w.wire_sc.ensure(lm * L.n * 32)) != MSM_OK)
+      if ((!shared && (rc = w.wire_pts.ensure((size_t)nm * n * 128)) != MSM_OK) ||
+          (rc = w.wire_sc.ensure((size_t)nm * n * 32)) != MSM_OK)
         return rc;
     }
   }
@@ -1508,18 +1475,17 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // number of real (not padding) MSMs in it.
   auto launch_inputs = [&](size_t j, BatchPtrs* bp, BatchPtrs* bs) -> uint32_t {
     Slot& sl = c->slot[j % nslot];
-    const LaunchSpec& L = ls[j];
-    const uint32_t lm = L.pl.d.nm, nreal = L.nreal;
+    const uint32_t nreal = (uint32_t)std::min<size_t>(nm, count - j * nm);
     *bp = BatchPtrs{};
     *bs = BatchPtrs{};
     for (uint32_t m = 0; m < MSM_MAX_BATCH; m++) {
-      const size_t b = L.first + std::min<uint32_t>(std::min<uint32_t>(m, lm - 1), nreal - 1);
+      const size_t b = std::min(j * nm + std::min<uint32_t>(m, nm - 1), count - 1);
       bp->p[m] = shared ? in.shared_points : in.points[b];
       bs->p[m] = in.scalars[b];
       if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
         const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
-        bs->p[m] = in.dev_scalars ? in.dev_scalars[L.first + mr] : sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * L.n * 8;
-        if (!shared) bp->p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * L.n * 32;
+        bs->p[m] = in.dev_scalars ? in.dev_scalars[j * nm + mr] : sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
+        if (!shared) bp->p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
       }
     }
     return nreal;
@@ -1534,16 +1500,14 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     Slot& sl = c->slot[j % nslot];
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
-    const LaunchSpec& L = ls[j];
-    const size_t n = L.n;  // this launch's MSM size
     auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
     auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
       for (uint32_t m0 = 0; m0 < nreal;) {
-        const size_t b0 = L.first + m0;
+        const size_t b0 = std::min(j * nm + m0, count - 1);
         const uint32_t* h0 = src[b0];
         uint32_t m1 = m0 + 1;
         if (len_of(b0) == n)
-          while (m1 < nreal && len_of(L.first + m1) == n && src[L.first + m1] == h0 + (size_t)(m1 - m0) * n * per) m1++;
+          while (m1 < nreal && len_of(j * nm + m1) == n && src[j * nm + m1] == h0 + (size_t)(m1 - m0) * n * per) m1++;
         const size_t words = (m1 - m0 == 1 ? len_of(b0) : (size_t)(m1 - m0) * n) * per;
         if (words && hipMemcpyAsync(const_cast<uint32_t*>(dst.p[m0]), h0, words * 4, hipMemcpyHostToDevice,
                                     c->copy_stream) != hipSuccess)
@@ -1554,7 +1518,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     };
     if (!in.dev_scalars && !up(in.scalars, bs, 8)) return MSM_ERR_HIP;
     for (uint32_t m = 0; m < nreal && !shared; m++) {
-      const size_t len = len_of(L.first + m);
+      const size_t len = len_of(std::min(j * nm + m, count - 1));
       if (len < n) {
         hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
                            const_cast<uint32_t*>(bp.p[m]) + len * 32, const_cast<uint32_t*>(bs.p[m]) + len * 8,
@@ -1633,7 +1597,6 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       Slot& sl = c->slot[si];
       BatchPtrs bp, bs;
       launch_inputs(j, &bp, &bs);
-      const Plan& pl = ls[j].pl;
       const int parts = shared ? (PART_SORT | PART_ACC | PART_POST) : PART_ALL;
       uint32_t* pts = shared ? pts_shared : sl.ws.pts.as<uint32_t>();
       // The last launch's bucket sort starts on its scalars while its points upload: the sort then
@@ -1658,14 +1621,13 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     if (have) {
       // the launch's window Horners side by side (one host thread per MSM): the last launch's are
       // the pipeline's drain, on the critical path of the call
-      const LaunchSpec& F = ls[f];
-      const uint32_t k = F.nreal;
+      const uint32_t k = (uint32_t)std::min<size_t>(nm, count - f * nm);
       Pt res[MSM_MAX_BATCH];
       std::thread th[MSM_MAX_BATCH];
-      for (uint32_t m = 1; m < k; m++) th[m] = std::thread([&, m] { res[m] = horner_tail(F.pl, terms.data(), m); });
-      res[0] = horner_tail(F.pl, terms.data(), 0);
+      for (uint32_t m = 1; m < k; m++) th[m] = std::thread([&, m] { res[m] = horner_tail(pl, terms.data(), m); });
+      res[0] = horner_tail(pl, terms.data(), 0);
       for (uint32_t m = 1; m < k; m++) th[m].join();
-      for (uint32_t m = 0; m < k; m++) emit(res[m], F.first + m);
+      for (uint32_t m = 0; m < k; m++) emit(res[m], f * nm + m);
     }
   }
   stop_uploader();  // its last copies were waited for by the last launch
@@ -1730,51 +1692,21 @@ bool host_scalars_first() {
   return on;
 }
 
-// The graded tail of a split host-input MSM: log2 sizes of the last slices, each its own launch on
-// its own plan, so that the compute left after the last upload is the smallest slice's
-// (MSM_HOST_TAIL="17,16,16"; unset or 0: none).
-std::vector<size_t> host_tail_sizes() {
-  static const std::vector<size_t> v = [] {
-    std::vector<size_t> r;
-    const char* e = getenv("MSM_HOST_TAIL");
-    if (!e) return r;
-    for (const char* q = e; *q;) {
-      const int lg = atoi(q);
-      if (lg >= 10 && lg <= 20) r.push_back((size_t)1 << lg);
-      while (*q >= '0' && *q <= '9') q++;
-      if (*q) q++;  // any separator: "17,16,16" or "17_16_16"
-    }
-    return r;
-  }();
-  return v;
-}
-
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
   // G <= 16 balanced slices of s points, a whole number of launches of nmb slices (every slice
   // is an MSM of s points to the pipelined entry; in.lens: a short slice is padded on the device
-  // with identity points and zero scalars, which add no bucket entries), then the graded tail's
-  // slices (host_tail_sizes), when they leave at least two body slices.
+  // with identity points and zero scalars, which add no bucket entries).  (Short tail slices for
+  // the last launch -- its compute is what is left after the last upload -- measured slower: one
+  // more launch costs more than the shorter tail saves)
   const uint32_t nmb = host_batch();
-  std::vector<size_t> tail = host_tail_sizes();
-  size_t tsum = 0;
-  for (size_t t : tail) tsum += t;
-  if (tsum + 2 * host_piece() > n) {
-    tail.clear();
-    tsum = 0;
-  }
-  const size_t nb = n - tsum;  // the body's points
-  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, nb / host_piece()));
+  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, n / host_piece()));
   Gb = (Gb + nmb - 1) / nmb * nmb;
-  const size_t s = (nb + Gb - 1) / Gb;
+  const size_t s = (n + Gb - 1) / Gb;
   std::vector<size_t> offs, lens;
   for (size_t g = 0; g < Gb; g++) {
-    offs.push_back(std::min(g * s, nb));
-    lens.push_back(g * s < nb ? std::min(s, nb - g * s) : 0);  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
-  }
-  for (size_t k = 0, at = nb; k < tail.size(); at += tail[k], k++) {
-    offs.push_back(at);
-    lens.push_back(tail[k]);
+    offs.push_back(std::min(g * s, n));
+    lens.push_back(g * s < n ? std::min(s, n - g * s) : 0);  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
   }
   const size_t G = offs.size();
   std::vector<const uint32_t*> pp(G), ss(G);
@@ -1788,31 +1720,26 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   in.scalars = ss.data();
   in.batch = nmb;
   in.lens = lens.data();
-  in.tail_n = tail.empty() ? nullptr : tail.data();
-  in.tail_count = tail.size();
   std::vector<const uint32_t*> dsc(G);
   if (host_scalars_first()) {
-    // body slice g's scalars at g s in one device buffer (s words each, the tail of a short slice
-    // is its device padding), the graded tail's after them: the run of slices that lie in the
-    // buffer as in the caller's array goes up in one copy, every other slice in its own
-    if (int rc = c->host_sc.ensure((Gb * s + tsum) * 32)) return rc;
+    // slice g's scalars at g s in one device buffer (s words each, the tail of a short slice is
+    // its device padding): the run of full slices at the front goes up in one copy, every other
+    // slice in its own
+    if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
     uint32_t* base = c->host_sc.as<uint32_t>();
-    std::vector<size_t> at(G);
-    for (size_t g = 0; g < G; g++) at[g] = g < Gb ? g * s : Gb * s + (offs[g] - nb);
     for (size_t g = 0; g < G;) {
       size_t h = g + 1;
-      while (h < G && lens[h - 1] == (h - 1 < Gb ? s : lens[h - 1]) && at[h] == at[g] + (offs[h] - offs[g]) &&
-             offs[h] == offs[h - 1] + lens[h - 1])
-        h++;
-      const size_t words = (offs[h - 1] + lens[h - 1] - offs[g]) * 8;
-      if (words && hipMemcpyAsync(base + at[g] * 8, scalars_be + offs[g] * 8, words * 4, hipMemcpyHostToDevice,
+      if (lens[g] == s)
+        while (h < G && lens[h] == s && offs[h] == offs[g] + (h - g) * s) h++;
+      const size_t words = (h - g == 1 ? lens[g] : (h - g) * s) * 8;
+      if (words && hipMemcpyAsync(base + g * s * 8, scalars_be + offs[g] * 8, words * 4, hipMemcpyHostToDevice,
                                   c->copy_stream) != hipSuccess) {
         hipStreamSynchronize(c->copy_stream);
         return MSM_ERR_HIP;
       }
       g = h;
     }
-    for (size_t g = 0; g < G; g++) dsc[g] = base + at[g] * 8;
+    for (size_t g = 0; g < G; g++) dsc[g] = base + g * s * 8;
     in.dev_scalars = dsc.data();
   }
   std::vector<Pt> part(G, pt_identity());
