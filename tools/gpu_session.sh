@@ -44,6 +44,7 @@
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
 #   set:VAR=VAL / unset:VAR  environment for the steps that follow (e.g. set:MSM_RED_L=8 kstats1)
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
+#   ldshist      the sort's LDS counting atomics under random, bank-spread and equal keys
 set -u
 [ $# -ge 2 ] || { awk 'NR > 1 && /^#/ { print; next } NR > 1 { exit }' "$0"; exit 2; }
 TAG=$1; shift
@@ -221,6 +222,7 @@ for step in "$@"; do
     ubench)
       run ubench_fmul 120 tools/ubench/fmul_bench
       run ubench_isa 120 tools/ubench/isa_rates ;;
+    ldshist) run ldshist 120 tools/ubench/lds_hist ;;  # LDS counting atomics: random / spread / same keys
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
