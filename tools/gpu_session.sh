@@ -39,6 +39,7 @@
 #                under webgpu-msm_amd/msm_amd/_lib), R rounds (default 3); $BENCH_X adds bench.py
 #                arguments and $KS suffixes the output names
 #   env:VAR=A,B[:R]  the same A/B over values of one environment knob (e.g. env:MSM_FORK_PREP=0,1)
+#   envsize:LG:VAR=A,B[:R]  the same at 2^LG points (no extras)
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
 #   latlib:LIBS[:R]  single-MSM latency over in-tree library variants
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
@@ -190,6 +191,17 @@ for step in "$@"; do
         for v in ${vals//,/ }; do
           export "$var=$v"
           run "env_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          unset "$var"
+        done
+      done ;;
+    envsize:*)  # envsize:LG:VAR=A,B[:R] -- env:VAR=A,B at 2^LG points
+      IFS=: read -r _ lg spec rounds <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for r in $(seq 1 "${rounds:-2}"); do
+        for v in ${vals//,/ }; do
+          export "$var=$v"
+          run "envsize${lg}_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 --no-extras "${BENCH_Q[@]}" \
+            --n $((1 << lg))
           unset "$var"
         done
       done ;;
