@@ -221,6 +221,40 @@ def test_lone_msm_tail_threads_agree(n):
     assert got[0] == got[1] == got[3] == got[-3] == got[-1]
 
 
+@pytest.mark.parametrize("n,k", [(1 << 12, 2), (1 << 17, 2), (1 << 16, 4), (1 << 12, 1)])
+def test_batch_tail_matches_per_msm_horner(n, k):
+    """The last launch's tails of a pipelined run (TailCrew::run_batch: the window sums of all k
+    MSMs over the helpers, the outer Horners of MSMs 1.. taken by helpers) equal one horner_tail
+    per MSM, for 1, 2 and 3 helpers (fewer helpers than MSMs: the caller runs the outer Horners no
+    helper took), identity terms included."""
+    L = M.load()
+    words = L.msm_test_tail_words(n)
+    rng = np.random.default_rng(n + k)
+    terms = np.zeros(words * k, np.uint32)
+    for i in range(words * k // 32):
+        if i % 5 == 2:
+            x, y, z = 0, 1, 3
+        else:
+            x, y = O.scalar_mul(O.G, int(rng.integers(1, 1 << 30)))
+            z = int(rng.integers(1, 1 << 30))
+        for j, v in enumerate((x * z % O.P, y * z % O.P, x * y % O.P * z % O.P, z)):
+            terms[i * 32 + 8 * j: i * 32 + 8 * j + 8] = _host_mont_words(v)
+    got = {}
+    for helpers in (0, 1, 2, 3):
+        out = (ctypes.c_uint32 * (16 * k))()
+        ms = ctypes.c_double()
+        assert L.msm_test_tail_batch(n, k, terms.ctypes.data, helpers, out, ctypes.byref(ms)) == 0, helpers
+        got[helpers] = [(M.wire_to_int(out[16 * m: 16 * m + 8]), M.wire_to_int(out[16 * m + 8: 16 * m + 16]))
+                        for m in range(k)]
+    assert got[0] == got[1] == got[2] == got[3]
+    assert len(set(got[0])) == k  # the MSMs' blocks differ: each Horner read its own block
+    # the single-MSM entry on block 0 agrees
+    out = (ctypes.c_uint32 * 16)()
+    ms = ctypes.c_double()
+    assert L.msm_test_tail(n, terms.ctypes.data, 3, out, ctypes.byref(ms)) == 0
+    assert (M.wire_to_int(out[:8]), M.wire_to_int(out[8:])) == got[0][0]
+
+
 def test_host_inverse_matches_fermat():
     """hostfield.h's binary-Euclid fq_inv (the affine conversion's inverse) equals a^(p-2) and
     a * a^-1 = 1 on 4,000 pseudo-random full-width and short values, 1 and p - 1, and maps 0 to 0

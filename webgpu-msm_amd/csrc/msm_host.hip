@@ -762,48 +762,75 @@ class TailCrew {
   // The terms are on the host: the helpers start on the window sums, the caller on the outer
   // Horner, taking each window sum as it becomes ready (and computing one itself when none is).
   Pt run(const Plan& pl, const uint32_t* terms) {
+    Pt r;
+    run_batch(pl, terms, 1, &r);
+    return r;
+  }
+  // The same for the k MSMs of one launch (terms block m at m * Wr * nterms * 32 words): the window
+  // sums of all k, top windows first, over every thread; the outer Horner of MSM 0 on the caller,
+  // those of MSMs 1.. on the first helpers free (the caller runs any no helper took).
+  void run_batch(const Plan& pl, const uint32_t* terms, uint32_t k, Pt* out) {
     pl_ = &pl;
     terms_ = terms;
-    const uint32_t Wr = pl.d.Wr, w0 = pl.d.w0;  // local window w is window w0 + w of the MSM
-    sums_.assign(Wr, pt_identity());
-    ready_.reset(new std::atomic<int>[Wr]);
-    for (uint32_t w = 0; w < Wr; w++) ready_[w].store(0);
+    k_ = k;
+    out_ = out;
+    const uint32_t n = k * pl.d.Wr;
+    sums_.assign(n, pt_identity());
+    ready_.reset(new std::atomic<int>[n]);
+    for (uint32_t i = 0; i < n; i++) ready_[i].store(0);
+    odone_.reset(new std::atomic<int>[k]);
+    for (uint32_t m = 0; m < k; m++) odone_[m].store(0);
     next_.store(0);
+    next_outer_.store(1);
     go_.store(true, std::memory_order_release);
-    Pt acc = pt_identity();
-    bool any = false;
-    for (uint32_t k = 0; k < Wr; k++) {
-      const uint32_t w = Wr - 1 - k;
-      while (!ready_[w].load(std::memory_order_acquire))
-        if (!take_one()) _mm_pause();
-      const Pt& p = sums_[w];
-      const bool ident = fq_is_zero(p.X) && fq_eq(p.Y, p.Z);
-      if (!ident) acc = any ? pt_add(acc, p) : p;
-      any = any || !ident;
-      const uint32_t next = w ? win_off(pl.d, w0 + w - 1) : 0u;
-      if (any && win_off(pl.d, w0 + w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w0 + w) - next));
+    out[0] = outer(0);
+    for (uint32_t m; (m = next_outer_.fetch_add(1)) < k;) {
+      out[m] = outer(m);
+      odone_[m].store(1, std::memory_order_release);
     }
+    for (uint32_t m = 1; m < k; m++)
+      while (!odone_[m].load(std::memory_order_acquire))
+        if (!take_one()) _mm_pause();
     // every helper is out of this job before its state is reset by the next one
     armed_.store(false);
     wait_idle();
     go_.store(false);
-    return acc;
   }
 
  private:
   void wait_idle() {
     while (idle_.load(std::memory_order_acquire) < (int)th_.size()) _mm_pause();
   }
-  // One window sum, top window first; false when none is left.
+  // MSM m = sum_w 2^(off_w) W_w by Horner over its windows, top first, each window sum taken as it
+  // becomes ready (computing others meanwhile).
+  Pt outer(uint32_t m) {
+    const Plan& pl = *pl_;
+    const uint32_t Wr = pl.d.Wr, w0 = pl.d.w0;  // local window w is window w0 + w of the MSM
+    Pt acc = pt_identity();
+    bool any = false;
+    for (uint32_t kk = 0; kk < Wr; kk++) {
+      const uint32_t w = Wr - 1 - kk;
+      while (!ready_[m * Wr + w].load(std::memory_order_acquire))
+        if (!take_one()) _mm_pause();
+      const Pt& p = sums_[m * Wr + w];
+      const bool ident = fq_is_zero(p.X) && fq_eq(p.Y, p.Z);
+      if (!ident) acc = any ? pt_add(acc, p) : p;
+      any = any || !ident;
+      const uint32_t next = w ? win_off(pl.d, w0 + w - 1) : 0u;
+      if (any && win_off(pl.d, w0 + w) > next) acc = pt_dbl_n(acc, (int)(win_off(pl.d, w0 + w) - next));
+    }
+    return acc;
+  }
+  // One window sum, top windows (of every MSM) first; false when none is left.
   bool take_one() {
     const uint32_t Wr = pl_->d.Wr;
-    const uint32_t k = next_.fetch_add(1);
-    if (k >= Wr) return false;
-    const uint32_t w = Wr - 1 - k;
+    const uint32_t job = next_.fetch_add(1);
+    if (job >= k_ * Wr) return false;
+    const uint32_t m = job % k_, w = Wr - 1 - job / k_;
     std::vector<std::pair<uint32_t, const uint32_t*>> at;
-    collect_terms(*pl_, terms_, w, w + 1, win_off(pl_->d, pl_->d.w0 + w), &at);
-    sums_[w] = horner_run(at, term_at);
-    ready_[w].store(1, std::memory_order_release);
+    collect_terms(*pl_, terms_ + (size_t)m * Wr * pl_->nterms * 32, w, w + 1, win_off(pl_->d, pl_->d.w0 + w), &at);
+    sums_[m * Wr + w] = horner_run(at, term_at);
+    ready_[m * Wr + w].store(1, std::memory_order_release);
     return true;
   }
   void work() {
@@ -821,9 +848,14 @@ class TailCrew {
         if (++spins > 4096) std::this_thread::yield();
         else _mm_pause();
       }
-      if (go_.load(std::memory_order_acquire))
+      if (go_.load(std::memory_order_acquire)) {
+        for (uint32_t m; (m = next_outer_.fetch_add(1)) < k_;) {
+          out_[m] = outer(m);
+          odone_[m].store(1, std::memory_order_release);
+        }
         while (take_one()) {
         }
+      }
       idle_.fetch_add(1, std::memory_order_release);
     }
   }
@@ -833,11 +865,13 @@ class TailCrew {
   uint64_t gen_ = 0;
   std::atomic<bool> go_{false}, armed_{false}, quit_{false};
   std::atomic<int> idle_{1 << 30};  // helpers done with the current round (all idle at start)
-  std::atomic<uint32_t> next_{0};
+  std::atomic<uint32_t> next_{0}, next_outer_{1};
   const Plan* pl_ = nullptr;
   const uint32_t* terms_ = nullptr;
+  uint32_t k_ = 1;
+  Pt* out_ = nullptr;
   std::vector<Pt> sums_;
-  std::unique_ptr<std::atomic<int>[]> ready_;
+  std::unique_ptr<std::atomic<int>[]> ready_, odone_;
 };
 
 void pt_to_be_affine(const Pt& p, uint32_t out[16]) {
@@ -1556,7 +1590,13 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     up_stop.store(true);
     if (up_th.joinable()) up_th.join();
   };
+  // the device context's tail helpers take the last launch's host tails (armed once it is enqueued)
+  if (tail_helpers() > 0 && !c->crew) c->crew = new TailCrew(tail_helpers());
+  TailCrew* crew = tail_helpers() > 0 ? c->crew : nullptr;
+  bool crew_armed = false;
   auto fail = [&](int code) {
+    if (crew_armed) crew->disarm();  // no terms will come
+    crew_armed = false;
     stop_uploader();
     hipStreamSynchronize(c->copy_stream);
     for (int k = 0; k < nslot; k++) hipStreamSynchronize(c->slot[k].stream);
@@ -1617,16 +1657,26 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
         return fail(rc);
       enqueued.store(j + 1, std::memory_order_release);
+      if (crew && j + 1 == nbatch) {
+        crew->arm();  // spins while the device runs the last launch
+        crew_armed = true;
+      }
     }
     if (have) {
-      // the launch's window Horners side by side (one host thread per MSM): the last launch's are
-      // the pipeline's drain, on the critical path of the call
       const uint32_t k = (uint32_t)std::min<size_t>(nm, count - f * nm);
       Pt res[MSM_MAX_BATCH];
-      std::thread th[MSM_MAX_BATCH];
-      for (uint32_t m = 1; m < k; m++) th[m] = std::thread([&, m] { res[m] = horner_tail(pl, terms.data(), m); });
-      res[0] = horner_tail(pl, terms.data(), 0);
-      for (uint32_t m = 1; m < k; m++) th[m].join();
+      if (crew_armed && f + 1 == nbatch) {
+        // the last launch's tails are the pipeline's drain, on the critical path of the call: their
+        // window sums over the device context's helpers, the k outer Horners side by side
+        crew->run_batch(pl, terms.data(), k, res);
+        crew_armed = false;
+      } else {
+        // earlier launches' tails overlap the device's next launches: one host thread per MSM
+        std::thread th[MSM_MAX_BATCH];
+        for (uint32_t m = 1; m < k; m++) th[m] = std::thread([&, m] { res[m] = horner_tail(pl, terms.data(), m); });
+        res[0] = horner_tail(pl, terms.data(), 0);
+        for (uint32_t m = 1; m < k; m++) th[m].join();
+      }
       for (uint32_t m = 0; m < k; m++) emit(res[m], f * nm + m);
     }
   }
@@ -2414,6 +2464,27 @@ int msm_test_host_timing(int what, size_t iters, double* ns) {
 }
 
 // The number of window-term words msm_test_tail reads for n points.
+// msm_test_tail over k MSMs' terms at once (k blocks of msm_test_tail_words(n) words), as the last
+// launch of a pipelined run finishes: helpers > 0 runs TailCrew::run_batch on a crew of that many
+// threads, helpers = 0 one horner_tail per MSM.  out_xy_be: k affine results (16 words each).
+int msm_test_tail_batch(size_t n, uint32_t k, const uint32_t* terms, int helpers, uint32_t* out_xy_be, double* ms) {
+  if (!terms || !out_xy_be || !ms || k < 1 || k > MSM_MAX_BATCH || helpers < 0) return MSM_ERR_INVALID_ARG;
+  Plan pl;
+  if (int rc = make_plan(n, nullptr, DevShape{}, &pl)) return rc;
+  TailCrew crew(helpers);
+  Pt r[MSM_MAX_BATCH];
+  const auto t0 = clk::now();
+  if (helpers) {
+    crew.arm();
+    crew.run_batch(pl, terms, k, r);
+  } else {
+    for (uint32_t m = 0; m < k; m++) r[m] = horner_tail(pl, terms, m);
+  }
+  *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  for (uint32_t m = 0; m < k; m++) pt_to_be_affine(r[m], out_xy_be + 16 * m);
+  return MSM_OK;
+}
+
 size_t msm_test_tail_words(size_t n) {
   Plan pl;
   if (make_plan(n, nullptr, DevShape{}, &pl)) return 0;

@@ -132,6 +132,7 @@ def load() -> ctypes.CDLL:
                               u32p], ctypes.c_int),
         "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_tail_words": ([sz], sz),
+        "msm_test_tail_batch": ([sz, ctypes.c_uint32, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_peer_state": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     }
