@@ -41,6 +41,7 @@ extern "C" {
 #define MSM_FLAG_SERIAL 1u  /* pipelined entries: one launch in flight at a time (no overlap)     */
 #define MSM_FLAG_DEVICES 2u /* the device-list fields (devices, n_devices) are set: see below     */
 #define MSM_FLAG_WINDOWS 4u /* the window-range fields (window_lo, window_hi) are set: see below  */
+#define MSM_FLAG_HALF_WINDOWS 8u /* with MSM_FLAG_WINDOWS: window_lo / window_hi count half windows */
 
 #define MSM_MAX_DEVICES 16
 
@@ -84,7 +85,11 @@ typedef struct msm_opts {
  * so the window ranges are a second way to shard one MSM over devices besides the point vector:
  * every device then reads all n points and scalars but does 1/D of the bucket work and of the
  * reduction.  Meant for the *_partial entries; window_bits 0, an empty range or one
- * past the last window give MSM_ERR_INVALID_ARG. */
+ * past the last window give MSM_ERR_INVALID_ARG.
+ * With MSM_FLAG_HALF_WINDOWS the range is counted in half windows, [0, 2 msm_window_count(c)):
+ * half window 2w is window w's buckets of the lower half of its digit magnitudes, 2w + 1 the upper
+ * half, so a range may start or end in the middle of a window (an odd number of windows can be
+ * cut into equal shares). */
 uint32_t msm_window_count(uint32_t window_bits);
 
 /* Per-phase device times (ms) of the most recent MSM on the calling thread's device when

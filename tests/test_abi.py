@@ -127,9 +127,11 @@ def test_opts_struct_layout_matches_header():
     assert ctypes.sizeof(M.MsmOpts) == 40
     assert M.MsmOpts.devices.offset == 16 and M.MsmOpts.n_devices.offset == 24
     assert M.MsmOpts.window_lo.offset == 32 and M.MsmOpts.window_hi.offset == 36
-    flags = dict(re.findall(r"#define (MSM_FLAG_[A-Z]+) (\d+)u", src))
+    flags = dict(re.findall(r"#define (MSM_FLAG_[A-Z_]+) (\d+)u", src))
     assert int(flags["MSM_FLAG_SERIAL"]) == M.MSM_FLAG_SERIAL and int(flags["MSM_FLAG_DEVICES"]) == M.MSM_FLAG_DEVICES
     assert int(flags["MSM_FLAG_WINDOWS"]) == M.MSM_FLAG_WINDOWS
+    assert int(flags["MSM_FLAG_HALF_WINDOWS"]) == M.MSM_FLAG_HALF_WINDOWS
+    assert len(set(flags.values())) == len(flags)  # distinct bits
     assert int(re.search(r"#define MSM_MAX_DEVICES (\d+)", src).group(1)) == M.MSM_MAX_DEVICES
 
 

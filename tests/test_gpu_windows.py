@@ -2,7 +2,9 @@
 windows [lo, hi) returns sum over those windows of 2^(offset w) G_w, so the partials of a partition
 of the windows join (projective adds, msm_combine_partials) into the whole MSM -- the second way of
 sharding one MSM over devices.  Every result is checked against the closed form
-sum_i s_i (k_i G) = ((sum s_i k_i) mod r) G, including full 256-bit scalars (the overflow window)."""
+sum_i s_i (k_i G) = ((sum s_i k_i) mod r) G, including full 256-bit scalars (the overflow window).
+Half-window ranges (MSM_FLAG_HALF_WINDOWS, (lo, hi, 2)) cut a window between the lower and upper
+halves of its bucket magnitudes: their partitions join the same way."""
 import numpy as np
 import pytest
 
@@ -80,4 +82,58 @@ def test_bad_window_ranges_rejected(c, rng):
     pts, sc = M.gen_points(64), M.gen_scalars(64)
     with pytest.raises(M.MsmError) as e:
         M.compute_msm_partial(pts, sc, window_size=c or None, windows=rng)
+    assert e.value.code == -1
+
+
+@pytest.mark.parametrize("n,c,cuts", [
+    (1000, 10, [11]),                      # window 5 split in its middle
+    (70001, 13, [1, 2, 7, 20, 39]),        # odd cuts everywhere, the overflow window halved too
+    ((1 << 17) + 3, 15, [17]),             # the 8-GPU split's 8.5 / 8.5 windows
+    ((1 << 18), 15, [9, 17, 26]),          # four half-window ranges
+])
+@pytest.mark.parametrize("full", [False, True])
+def test_half_window_partition_joins_to_msm(n, c, cuts, full):
+    pts = M.gen_points(n, k0=5, step=3)
+    sc = _full_scalars(n, n + c + 1) if full else M.gen_scalars(n, seed=n + c + 1)
+    exp = closed_form(5, 3, sc)
+    wm = M.window_count(c)
+    rs = [(lo, hi, 2) for lo, hi in _ranges(2 * wm, cuts)]
+    host = [M.compute_msm_partial(pts, sc, window_size=c, windows=r) for r in rs]
+    assert M.combine_partials(np.stack(host)) == exp, rs
+    dp, ds = _dev(pts), _dev(sc)
+    dev = [M.compute_msm_device_partial(dp, ds, n, window_size=c, windows=r) for r in rs]
+    assert M.combine_partials(np.stack(dev)) == exp, rs
+    # whole windows in half units (even edges): the whole MSM (affine; the projective form depends
+    # on the order the atomics place a bucket's entries in)
+    assert M.combine_partials(M.compute_msm_partial(pts, sc, window_size=c, windows=(0, 2 * wm, 2)).reshape(1, 32)) == exp
+
+
+def test_pipelined_half_window_split():
+    """The rank/device split's share: 2^17-point shards x the two half-window ranges of c = 15
+    (msm_amd.dist.split_part), pipelined K MSMs per share, joined per MSM."""
+    from msm_amd.dist import split_part
+
+    n, K, world = 1 << 18, 5, 4
+    pts = M.gen_points(n, k0=2, step=5)
+    scs = [M.gen_scalars(n, seed=1200 + j) for j in range(K)]
+    exps = [closed_form(2, 5, s) for s in scs]
+    parts = []
+    for rank in range(world):
+        lo, hi, win, c = split_part(n, rank, world, "2x2")
+        assert win is not None and len(win) == 3
+        dp = _dev(pts[lo:hi])
+        dss = [_dev(s[lo:hi]) for s in scs]
+        parts.append(M.compute_msm_many_device_partial([dp] * K, dss, hi - lo, window_size=c, windows=win))
+    assert M.combine_partials_many(np.stack(parts)) == exps
+
+
+@pytest.mark.parametrize("rng", [(0, 37, 2), (5, 5, 2), (7, 3, 2), (0, 2, 3)])
+def test_bad_half_window_ranges_rejected(rng):
+    pts, sc = M.gen_points(64), M.gen_scalars(64)
+    if rng[2] == 3:
+        with pytest.raises(ValueError):
+            M.compute_msm_partial(pts, sc, window_size=15, windows=rng)
+        return
+    with pytest.raises(M.MsmError) as e:
+        M.compute_msm_partial(pts, sc, window_size=15, windows=rng)  # 2 * 18 = 36 half windows at c = 15
     assert e.value.code == -1

@@ -5,23 +5,28 @@ tests/test_gpu_windows.py; here: every (point, window) pair is computed exactly 
 import pytest
 
 import msm_amd as M
-from msm_amd.dist import SPLIT_WINDOW_BITS, parse_split, shard_range, split_part, window_ranges
+from msm_amd.dist import SPLIT_HALF_WINDOWS, SPLIT_WINDOW_BITS, parse_split, shard_range, split_part, window_ranges
 
 
 @pytest.mark.parametrize("c", range(4, 21))
 @pytest.mark.parametrize("q", range(1, 9))
-def test_window_ranges_cover_and_balance(c, q):
+@pytest.mark.parametrize("halves", [False, True])
+def test_window_ranges_cover_and_balance(c, q, halves):
     wm = M.window_count(c)
-    rs = window_ranges(wm, q)
+    u = 2 if halves else 1
+    rs = window_ranges(wm, q, halves)
     assert len(rs) == q
-    # contiguous, starting at 0, ending at wm (the overflow window wm - 1 in the top range)
-    assert rs[0][0] == 0 and rs[-1][1] == wm
+    assert all(len(r) == (3 if halves else 2) and (not halves or r[2] == 2) for r in rs)
+    # contiguous, starting at 0, ending at u wm (the overflow window in the top range)
+    assert rs[0][0] == 0 and rs[-1][1] == u * wm
     assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
-    assert all(lo < hi for lo, hi in rs)
-    # the wm - 1 main windows balanced: range sizes (overflow window aside) differ by at most one
-    sizes = [hi - lo for lo, hi in rs]
-    sizes[-1] -= 1
+    assert all(r[0] < r[1] for r in rs)
+    # the main windows balanced: range sizes (overflow window aside) differ by at most one unit
+    sizes = [r[1] - r[0] for r in rs]
+    sizes[-1] -= u
     assert max(sizes) - min(sizes) <= 1
+    if halves and q == 2:
+        assert sizes[0] == sizes[1]  # any main-window count splits evenly in half windows
 
 
 def test_parse_split():
@@ -50,7 +55,8 @@ def test_split_part_covers_every_point_and_window_once(world, split, n):
             assert win is None and cw is None
             win = (0, 1)  # all windows, one token
         else:
-            assert cw == SPLIT_WINDOW_BITS and 0 <= win[0] < win[1] <= wm
+            units = 2 if len(win) > 2 else 1
+            assert cw == SPLIT_WINDOW_BITS and 0 <= win[0] < win[1] <= units * wm
         key = (lo, hi)
         seen.setdefault(key, []).append(tuple(win))
     # P disjoint point shards covering [0, n), each split into the same complete window partition
@@ -61,4 +67,4 @@ def test_split_part_covers_every_point_and_window_once(world, split, n):
         wins.sort()
         assert len(wins) == Q
         if Q > 1:
-            assert wins == window_ranges(wm, Q)
+            assert wins == window_ranges(wm, Q, SPLIT_HALF_WINDOWS)

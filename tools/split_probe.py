@@ -5,7 +5,8 @@ measured on ONE GPU.
 
 A split P x Q (P * Q = D) gives GPU (p, q) the p-th contiguous 1/P of the points and the q-th of Q
 window ranges (msm_opts MSM_FLAG_WINDOWS; contiguous ranges of the msm_window_count(c) windows,
-balanced by main-window count, the overflow window with the top range).  For each split this
+balanced by main-window count, the overflow window with the top range; cut at half windows,
+MSM_FLAG_HALF_WINDOWS, unless --whole-windows).  For each split this
 runs every one of the D virtual GPUs' work in turn on the one GPU -- K pipelined MSMs of its shard
 and range through msm_compute_many_device_partial, device-resident inputs, exactly what that GPU
 would run -- times each (wall, K MSMs, after a warm-up), and joins all D x K partials on the host:
@@ -33,11 +34,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--window", type=int, default=0, help="window width for the window-split runs (0: 16)")
     ap.add_argument("--splits", default="", help="comma-separated PxQ (default: every factorisation of --gpus)")
+    ap.add_argument("--whole-windows", action="store_true",
+                    help="cut the window ranges at whole windows (default: half windows, as split_part)")
     a = ap.parse_args()
     import torch
 
     import msm_amd as M
-    from msm_amd.dist import shard_range, window_ranges
+    from msm_amd.dist import SPLIT_HALF_WINDOWS, shard_range, window_ranges
 
     D, n, K = a.gpus, a.n, a.steps
     with open(os.path.join(ROOT, "tests", "golden", "bench_expected.json")) as f:
@@ -52,7 +55,7 @@ def main():
     for P, Q in splits:
         c = a.window or (16 if Q > 1 else 0)  # point shards alone keep the tuned (pipelined) width
         wm = M.window_count(c) if c else None
-        ranges = window_ranges(wm, Q) if Q > 1 else [None]
+        ranges = window_ranges(wm, Q, SPLIT_HALF_WINDOWS and not a.whole_windows) if Q > 1 else [None]
         per_gpu, parts = [], []
         js = [s % sets for s in range(K)]
         for p in range(P):

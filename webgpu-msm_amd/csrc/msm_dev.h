@@ -27,6 +27,8 @@ struct MsmDims {
   uint32_t Wm;     // windows per MSM, overflow window included (all of them are recoded)
   uint32_t w0;     // window range of this launch (msm_opts MSM_FLAG_WINDOWS): windows
   uint32_t Wr;     //   [w0, w0 + Wr) of every MSM; local window l of an MSM is window w0 + l
+  uint32_t half_lo;  // MSM_FLAG_HALF_WINDOWS: local window 0 keeps only its upper-half buckets,
+  uint32_t half_hi;  //   local window Wr - 1 only its lower-half buckets (digit magnitudes)
   uint32_t nm;     // MSMs in the batch
   uint32_t q;      // main-window base width
   uint32_t nhi;    // main windows of width q + 1

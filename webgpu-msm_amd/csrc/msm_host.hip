@@ -134,6 +134,7 @@ struct Plan {
 bool plan_eq(const Plan& a, const Plan& b) {
   const MsmDims &x = a.d, &y = b.d;
   return x.n == y.n && x.c == y.c && x.B == y.B && x.W == y.W && x.Wm == y.Wm && x.w0 == y.w0 && x.Wr == y.Wr &&
+         x.half_lo == y.half_lo && x.half_hi == y.half_hi &&
          x.nm == y.nm && x.q == y.q &&
          x.nhi == y.nhi && x.fb == y.fb && x.nbc == y.nbc && x.nbins == y.nbins && x.ch == y.ch && x.nch == y.nch &&
          x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L &&
@@ -411,11 +412,17 @@ int make_plan(size_t n, const msm_opts* o, const DevShape& sh, Plan* pl, bool pi
   d.nm = nm;
   d.w0 = 0;
   d.Wr = d.Wm;
+  d.half_lo = d.half_hi = 0;
   if (o && (o->flags & MSM_FLAG_WINDOWS)) {
     // a window range needs an explicit width, so that every caller's ranges cut the same windows
-    if (!o->window_bits || o->window_lo >= o->window_hi || o->window_hi > d.Wm) return MSM_ERR_INVALID_ARG;
-    d.w0 = o->window_lo;
-    d.Wr = o->window_hi - o->window_lo;
+    const uint32_t units = (o->flags & MSM_FLAG_HALF_WINDOWS) ? 2u : 1u;
+    if (!o->window_bits || o->window_lo >= o->window_hi || o->window_hi > units * d.Wm) return MSM_ERR_INVALID_ARG;
+    d.w0 = o->window_lo / units;
+    d.Wr = (o->window_hi + units - 1) / units - d.w0;
+    if (units == 2) {
+      d.half_lo = o->window_lo & 1u;  // starts at window w0's upper half
+      d.half_hi = o->window_hi & 1u;  // ends after window w0 + Wr - 1's lower half
+    }
   }
   d.W = d.Wr * nm;
   d.c = d.nhi ? d.q + 1 : d.q;

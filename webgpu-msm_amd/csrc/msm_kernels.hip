@@ -337,6 +337,12 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
       uint32_t code = DigitCode<T>::ZERO;
       if (digit != 0) {
         const uint32_t mag = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
+        // half windows at the range's ends: a bucket outside the kept half is another share's
+        const uint32_t hb = 1u << (win_bits(d, wa) - 2);
+        if ((w == 0 && d.half_lo && mag < hb) || (w + 1 == d.Wr && d.half_hi && mag >= hb)) {
+          digits[(size_t)(w0 + w) * d.n + i] = (T)code;
+          return;
+        }
         code = mag | (digit < 0 ? DigitCode<T>::SIGN : 0u);
         atomicAdd(&lds_hist[w * d.nbc + (mag >> d.fb)], 1u);
       }

@@ -24,7 +24,7 @@ __all__ = [
     "compute_msm_shared_device", "compute_msm_many", "compute_msm_shared", "compute_msm_cpu", "MSM_FLAG_SERIAL",
     "combine_partials", "combine_partials_many", "point_add_affine",
     "split_dynamic", "get_best_window_size", "set_profiling", "last_profile", "device_count", "device_ordinals",
-    "MSM_FLAG_DEVICES", "MSM_FLAG_WINDOWS", "MSM_MAX_DEVICES", "window_count",
+    "MSM_FLAG_DEVICES", "MSM_FLAG_WINDOWS", "MSM_FLAG_HALF_WINDOWS", "MSM_MAX_DEVICES", "window_count",
     "lib_path", "points_to_wire", "scalars_to_wire", "wire_to_int", "P",
 ]
 
@@ -63,6 +63,7 @@ class MsmProfile(ctypes.Structure):
 MSM_FLAG_SERIAL = 1  # pipelined entries: one launch in flight at a time
 MSM_FLAG_DEVICES = 2  # msm_opts carries a device list (include/msm.h)
 MSM_FLAG_WINDOWS = 4  # msm_opts carries a window range
+MSM_FLAG_HALF_WINDOWS = 8  # with MSM_FLAG_WINDOWS: the range counts half windows
 MSM_MAX_DEVICES = 16
 MSM_STREAM_NULL = 1  # hip_stream value: order after the null (legacy default) stream
 
@@ -176,11 +177,17 @@ def _opts(window_size: Optional[int], run_length: Optional[int] = None, device: 
     """A msm_opts by reference.  `devices` (a list of HIP ordinals) runs the call on several
     devices (MSM_FLAG_DEVICES); the array is kept alive by the returned object.  `windows` =
     (lo, hi) restricts the MSM to those signed-digit windows (MSM_FLAG_WINDOWS; needs an explicit
-    window_size)."""
+    window_size); (lo, hi, 2) counts the range in half windows (MSM_FLAG_HALF_WINDOWS: half window
+    2w is window w's lower-half buckets, 2w + 1 its upper half)."""
     o = MsmOpts(int(window_size or 0), int(run_length or 0), int(device), int(flags))
     if windows is not None:
         o.window_lo, o.window_hi = int(windows[0]), int(windows[1])
         o.flags |= MSM_FLAG_WINDOWS
+        if len(windows) > 2:
+            if int(windows[2]) not in (1, 2):
+                raise ValueError(f"window range unit 1/{windows[2]}: only whole (1) or half (2) windows")
+            if int(windows[2]) == 2:
+                o.flags |= MSM_FLAG_HALF_WINDOWS
     if devices is not None:
         arr = (ctypes.c_int32 * max(len(devices), 1))(*[int(d) for d in devices])
         o.devices = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))

@@ -28,13 +28,21 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
 SPLIT_WINDOW_BITS = 15
 
 
-def window_ranges(wm: int, q: int):
+# Window splits cut in half windows (MSM_FLAG_HALF_WINDOWS): c = 15's 17 main windows then split
+# 8.5 / 8.5 instead of 8 / 9 between two ranges.
+SPLIT_HALF_WINDOWS = True
+
+
+def window_ranges(wm: int, q: int, halves: bool = False):
     """q contiguous ranges of an MSM's wm signed-digit windows: the wm - 1 main windows balanced,
-    the overflow window (empty for canonical scalars) with the top range."""
-    main = wm - 1
+    the overflow window (empty for canonical scalars) with the top range.  With `halves` the
+    ranges are counted in half windows, (lo, hi, 2) over [0, 2 wm), so an odd number of main
+    windows still splits evenly."""
+    u = 2 if halves else 1
+    main = u * (wm - 1)
     edges = [round(main * i / q) for i in range(q + 1)]
-    edges[-1] = wm
-    return list(zip(edges[:-1], edges[1:]))
+    edges[-1] = u * wm
+    return [(a, b, 2) if halves else (a, b) for a, b in zip(edges[:-1], edges[1:])]
 
 
 def parse_split(split: str, world: int) -> Tuple[int, int]:
@@ -50,8 +58,8 @@ def parse_split(split: str, world: int) -> Tuple[int, int]:
 
 def split_part(n: int, rank: int, world: int, split: str = "points"):
     """What GPU `rank` computes of an n-point MSM under a points x windows split: its point shard
-    [lo, hi), its window range (None: all windows) and the window width the range refers to (None:
-    the library's own choice).  Rank r takes point shard r // Q and window range r % Q; the partials
+    [lo, hi), its window range (None: all windows; (lo, hi, 2) in half windows) and the window
+    width the range refers to (None: the library's own choice).  Rank r takes point shard r // Q and window range r % Q; the partials
     of all ranks sum to the MSM."""
     from . import window_count
 
@@ -60,7 +68,7 @@ def split_part(n: int, rank: int, world: int, split: str = "points"):
     if Q == 1:
         return lo, hi, None, None
     c = SPLIT_WINDOW_BITS
-    return lo, hi, window_ranges(window_count(c), Q)[rank % Q], c
+    return lo, hi, window_ranges(window_count(c), Q, SPLIT_HALF_WINDOWS)[rank % Q], c
 
 
 def gather_partials(partial_xyzt_be: np.ndarray, device=None, group=None) -> np.ndarray:
