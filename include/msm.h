@@ -134,6 +134,18 @@ uint32_t msm_best_window(size_t n);
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                 uint32_t out_xy_be[16]);
 
+/* compute_msm with the reference's CPU/GPU co-compute (?cpuWorkRatio, submission.ts:94-154):
+ * share = floor(cpu_work_ratio * n) points [0, share) run on the library's host Pippenger
+ * (msm_compute_cpu's, cpu_threads threads, <= 0 = all hardware threads, its own window) on a
+ * thread of their own while points [share, n) run as msm_compute(opts) on the GPU(s); the two
+ * results join with one EC add (point_add_affine, lib.rs:240-253).  cpu_work_ratio 0 (or a share
+ * that floors to 0) is msm_compute; a share >= n is the reference's CPU-only branch.  Still a device
+ * entry: MSM_ERR_NO_DEVICE without a gfx950.  A negative or NaN ratio gives MSM_ERR_INVALID_ARG.
+ * The result equals msm_compute's for every ratio; on MI355X any share > ~0.1% delays it (the host
+ * runs a 2^20 MSM ~800x slower than one GPU), so this exists for interface parity. */
+int msm_compute_cocompute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                          double cpu_work_ratio, int cpu_threads, uint32_t out_xy_be[16]);
+
 /* Same with inputs already in device memory (device pointers, wire layout).  `hip_stream` may be
  * NULL or a hipStream_t: the library's streams then wait for the work enqueued on it so far (the
  * inputs it produces), and the call returns when the result is on the host.  With NULL the

@@ -61,6 +61,18 @@ def test_init_reports_device_state():
         with pytest.raises(M.MsmError) as e:
             M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]))
         assert e.value.code == -6
+        for ratio in (0.5, 1.0):  # the co-compute entry too, even when the host would take every point
+            with pytest.raises(M.MsmError) as e:
+                M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]), cpu_work_ratio=ratio)
+            assert e.value.code == -6
+
+
+@pytest.mark.parametrize("ratio", [-0.5, float("nan"), float("-inf")])
+def test_cocompute_rejects_bad_ratio(ratio):
+    """msm_compute_cocompute checks cpu_work_ratio before anything else (no GPU needed)."""
+    with pytest.raises(M.MsmError) as e:
+        M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]), cpu_work_ratio=ratio)
+    assert e.value.code == -1
 
 
 def test_strerror_and_best_window():

@@ -1,6 +1,7 @@
 """The TypeScript/JS drop-in (webgpu-msm_amd/js/submission.mjs) end to end on the GPU:
 compute_msm with BigIntPoint[]/bigint[] and U32ArrayPoint[]/Uint32Array[] inputs, and with
-flat wire buffers (the marshalling-free extension)."""
+flat wire buffers (the marshalling-free extension), and with { cpuWorkRatio } (the reference's
+CPU/GPU split, submission.ts:94-154: msm_compute_cocompute)."""
 import json
 import os
 import shutil
@@ -17,8 +18,9 @@ NODE = shutil.which("node")
 
 
 @pytest.mark.skipif(NODE is None, reason="node not installed")
-@pytest.mark.parametrize("form", ["bigint", "u32", "flat"])
-def test_compute_msm_js(form, tmp_path):
+@pytest.mark.parametrize("form,ratio", [("bigint", None), ("u32", None), ("flat", None), ("bigint", 0.3),
+                                        ("u32", 0.001), ("flat", 0.5), ("flat", 1.0)])
+def test_compute_msm_js(form, ratio, tmp_path):
     n = 500
     pts = O.gen_points(n, k0=21, step=13)
     ss = O.xorshift_scalars(n, seed=77)
@@ -43,7 +45,7 @@ if ("{form}" === "bigint") {{
   scalars = new Uint32Array(d.sc.length * 8);
   d.sc.forEach((v, i) => scalars.set(toWords(v), 8 * i));
 }}
-m.compute_msm(points, scalars).then((r) => console.log(r.x.toString() + "," + r.y.toString()),
+m.compute_msm(points, scalars, {json.dumps({"cpuWorkRatio": ratio} if ratio is not None else None)}).then((r) => console.log(r.x.toString() + "," + r.y.toString()),
   (e) => {{ console.error(e); process.exit(3); }});
 """
     path = tmp_path / "run_js.mjs"

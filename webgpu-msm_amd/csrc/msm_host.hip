@@ -2142,6 +2142,34 @@ int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n,
   return MSM_OK;
 }
 
+// CPU/GPU co-compute (submission.ts:94-154): the host Pippenger (msm_cpu.h) takes points
+// [0, share) on a thread of its own while the device path runs [share, n) as msm_compute, and the
+// two affine results join with one EC add (point_add_affine, lib.rs:240-253).
+int msm_compute_cocompute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
+                          double cpu_work_ratio, int cpu_threads, uint32_t out_xy_be[16]) {
+  if (!out_xy_be || ((!points_be || !scalars_be) && n) || !(cpu_work_ratio >= 0.0)) return MSM_ERR_INVALID_ARG;
+  // cpuShare = floor(cpuWorkRatio * n) (submission.ts:98); >= n is the reference's CPU-only branch
+  const double share_d = cpu_work_ratio * (double)n;
+  const size_t share = share_d >= (double)n ? n : (size_t)share_d;
+  if (share == 0) return msm_compute(points_be, scalars_be, n, opts, out_xy_be);
+  int rc = msm_init();  // a device entry all the same: no gfx950, no result (the CPU-only entry is msm_compute_cpu)
+  if (rc != MSM_OK) return rc;
+  uint32_t cpu_xy[16];
+  int cpu_rc = MSM_OK;
+  std::thread cpu([&] { cpu_rc = cpu_msm(points_be, scalars_be, share, 0, cpu_threads, cpu_xy); });
+  Pt r = pt_identity();
+  if (share < n) rc = multi_host_entry(points_be + 32 * share, scalars_be + 8 * share, n - share, opts, &r);
+  cpu.join();
+  if (rc != MSM_OK) return rc;
+  if (cpu_rc != MSM_OK) return cpu_rc;
+  uint64_t x[4], y[4];
+  be_words_to_std(cpu_xy, x);
+  be_words_to_std(cpu_xy + 8, y);
+  r = pt_add(r, pt_from_affine_std(x, y));
+  pt_to_be_affine(r, out_xy_be);
+  return MSM_OK;
+}
+
 int msm_compute_partial(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                         uint32_t out_xyzt_be[32]) {
   if (!out_xyzt_be) return MSM_ERR_INVALID_ARG;

@@ -107,6 +107,7 @@ struct Job {
   size_t n = 0;
   uint32_t window = 0;
   std::vector<int32_t> devices;  // empty: the current device
+  double cpu_work_ratio = 0;     // > 0: CPU/GPU co-compute (msm_compute_cocompute)
   uint32_t out[16] = {0};
   int rc = 0;
 };
@@ -124,7 +125,8 @@ void execute(napi_env, void* data) {
   }
   const uint32_t* pts = j->p_points ? j->p_points : j->stage ? j->stage->points.data() : j->points.data();
   const uint32_t* sc = j->p_scalars ? j->p_scalars : j->stage ? j->stage->scalars.data() : j->scalars.data();
-  j->rc = msm_compute(pts, sc, j->n, &o, j->out);
+  j->rc = j->cpu_work_ratio != 0 ? msm_compute_cocompute(pts, sc, j->n, &o, j->cpu_work_ratio, 0, j->out)
+                                  : msm_compute(pts, sc, j->n, &o, j->out);
 }
 
 void complete(napi_env env, napi_status, void* data) {
@@ -198,6 +200,17 @@ bool get_devices(napi_env env, size_t argc, napi_value* argv, size_t at, std::ve
   return true;  // shape and ordinals are checked by libmsm (msm_opts, MSM_ERR_INVALID_ARG)
 }
 
+// Optional cpuWorkRatio (submission.ts:95-98): a number >= 0 (undefined / null: 0).  false on a bad value.
+bool get_ratio(napi_env env, size_t argc, napi_value* argv, size_t at, double* out) {
+  *out = 0;
+  if (argc <= at) return true;
+  napi_valuetype vt;
+  if (napi_typeof(env, argv[at], &vt) != napi_ok) return false;
+  if (vt == napi_undefined || vt == napi_null) return true;
+  if (vt != napi_number || napi_get_value_double(env, argv[at], out) != napi_ok) return false;
+  return *out >= 0;  // NaN and negatives rejected here (libmsm rejects them too)
+}
+
 uint32_t get_window(napi_env env, napi_value v) {
   napi_valuetype t;
   if (napi_typeof(env, v, &t) != napi_ok || t != napi_number) return 0;
@@ -207,22 +220,26 @@ uint32_t get_window(napi_env env, napi_value v) {
 }
 
 napi_value ComputeMsmU32(napi_env env, napi_callback_info info) {
-  size_t argc = 4;
-  napi_value argv[4];
+  size_t argc = 5;
+  napi_value argv[5];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   const uint32_t *pts, *sc;
   size_t plen, slen;
   bool pshared = false, sshared = false;
   std::vector<int32_t> devs;
+  double ratio = 0;
   if (argc < 2 || !get_u32_array(env, argv[0], &pts, &plen, &pshared) ||
-      !get_u32_array(env, argv[1], &sc, &slen, &sshared) || !get_devices(env, argc, argv, 3, &devs)) {
+      !get_u32_array(env, argv[1], &sc, &slen, &sshared) || !get_devices(env, argc, argv, 3, &devs) ||
+      !get_ratio(env, argc, argv, 4, &ratio)) {
     napi_throw_type_error(env, nullptr,
-                          "computeMsmU32(points: Uint32Array, scalars: Uint32Array, windowSize?, devices?: number[])");
+                          "computeMsmU32(points: Uint32Array, scalars: Uint32Array, windowSize?, devices?: number[], "
+                          "cpuWorkRatio?: number >= 0)");
     return nullptr;
   }
   Job* j = new Job();
   j->n = std::min(plen / 32, slen / 8);
   j->devices = std::move(devs);
+  j->cpu_work_ratio = ratio;
   if (pshared && sshared) {
     j->p_points = pts;
     j->p_scalars = sc;
@@ -259,8 +276,8 @@ bool bigint_be(napi_env env, napi_value v, uint32_t* out8) {
 }
 
 napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
-  size_t argc = 4;
-  napi_value argv[4];
+  size_t argc = 5;
+  napi_value argv[5];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   bool ap = false, as = false;
   if (argc < 2 || napi_is_array(env, argv[0], &ap) != napi_ok || !ap || napi_is_array(env, argv[1], &as) != napi_ok ||
@@ -272,9 +289,9 @@ napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
   NAPI_OK(napi_get_array_length(env, argv[0], &np_));
   NAPI_OK(napi_get_array_length(env, argv[1], &ns));
   Job* j = new Job();
-  if (!get_devices(env, argc, argv, 3, &j->devices)) {
+  if (!get_devices(env, argc, argv, 3, &j->devices) || !get_ratio(env, argc, argv, 4, &j->cpu_work_ratio)) {
     delete j;
-    napi_throw_type_error(env, nullptr, "devices must be an array of device ordinals");
+    napi_throw_type_error(env, nullptr, "devices must be an array of device ordinals, cpuWorkRatio a number >= 0");
     return nullptr;
   }
   j->n = std::min(np_, ns);

@@ -4,7 +4,8 @@ export type BigIntPoint = { x: bigint; y: bigint; t: bigint; z: bigint };
 export type U32ArrayPoint = { x: Uint32Array; y: Uint32Array; t: Uint32Array; z: Uint32Array };
 
 // Extensions: flat wire buffers (n x 32 / n x 8 BE words: the fast form, no per-point
-// marshalling) and options { windowSize, devices } (devices: gfx950 HIP ordinals to shard over).
+// marshalling) and options { windowSize, devices, cpuWorkRatio } (devices: gfx950 HIP ordinals to
+// shard over; cpuWorkRatio: the reference's CPU/GPU split, submission.ts:94-154).
 export declare const compute_msm: (
   baseAffinePoints: BigIntPoint[] | U32ArrayPoint[] | Uint32Array,
   scalars: bigint[] | Uint32Array[] | Uint32Array,

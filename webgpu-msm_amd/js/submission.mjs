@@ -15,9 +15,10 @@
 // argument { windowSize } or the MSM_WINDOW_SIZE environment variable.  { devices: [0, 1, ...] }
 // shards the MSM over those gfx950 devices inside this one call (one host thread and PCIe link
 // each, partials joined with one EC add each) -- the multi-device form of the reference's
-// CPU/GPU split (?cpuWorkRatio, submission.ts:96-154).  { cpuWorkRatio } itself is accepted and
-// the whole MSM runs on the GPU(s): the host would take ~1000x longer for its share, and the
-// result is the same.
+// CPU/GPU split.  { cpuWorkRatio } (or MSM_CPU_WORK_RATIO) is that split itself (?cpuWorkRatio,
+// submission.ts:94-154): the first floor(ratio n) points on libmsm's host Pippenger beside the GPU
+// share, joined with one EC add (msm_compute_cocompute).  Same result for every ratio; on MI355X
+// any share above ~0.1% only delays it (the host is ~800x slower than one GPU).
 // There is no WebGPU/WGSL/CPU fallback: without the addon or a gfx950 device this rejects.
 import { createRequire } from "module";
 import fs from "fs";
@@ -79,6 +80,12 @@ export function flattenU32(points, scalars) {
   return [pb, sb];
 }
 
+function ratioFrom(options) {
+  if (options && options.cpuWorkRatio !== undefined && options.cpuWorkRatio !== null) return Number(options.cpuWorkRatio);
+  const env = typeof process !== "undefined" && process.env ? process.env.MSM_CPU_WORK_RATIO : undefined;
+  return env ? parseFloat(env) : 0;
+}
+
 function devicesFrom(options) {
   if (!options || options.devices === undefined || options.devices === null) return undefined;
   if (!Array.isArray(options.devices)) throw new TypeError("options.devices must be an array of device ordinals");
@@ -88,11 +95,12 @@ function devicesFrom(options) {
 export const compute_msm = async (baseAffinePoints, scalars, options) => {
   const windowSize = windowFrom(options);
   const devices = devicesFrom(options);
+  const cpuWorkRatio = ratioFrom(options);
   if (baseAffinePoints instanceof Uint32Array && scalars instanceof Uint32Array) {
     // already flat wire buffers (x|y|t|z BE words per point, BE words per scalar): no marshalling
     const n = Math.min(Math.floor(baseAffinePoints.length / nUint32PerPoint), Math.floor(scalars.length / nUint32PerScalar));
     const result = await addon.computeMsmU32(baseAffinePoints.subarray(0, n * nUint32PerPoint),
-                                             scalars.subarray(0, n * nUint32PerScalar), windowSize, devices);
+                                             scalars.subarray(0, n * nUint32PerScalar), windowSize, devices, cpuWorkRatio);
     const [x, y] = u32ArrayToBigInts(result);
     return { x, y };
   }
@@ -104,10 +112,10 @@ export const compute_msm = async (baseAffinePoints, scalars, options) => {
     // native marshalling (napi_get_value_bigint_words) replaces convert_worker.ts
     const pts = typeof baseAffinePoints[0].x === "bigint" ? baseAffinePoints : baseAffinePoints.map(toBigIntPoint);
     const sc = typeof scalars[0] === "bigint" ? scalars : scalars.map((s) => u32ArrayToBigInts(s)[0]);
-    result = await addon.computeMsmBigInt(pts, sc, windowSize, devices);
+    result = await addon.computeMsmBigInt(pts, sc, windowSize, devices, cpuWorkRatio);
   } else {
     const [pointBuffer, scalarBuffer] = flattenU32(baseAffinePoints, scalars);
-    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize, devices);
+    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize, devices, cpuWorkRatio);
   }
   const [x, y] = u32ArrayToBigInts(result);
   return { x, y };

@@ -116,6 +116,7 @@ def load() -> ctypes.CDLL:
         "msm_compute_many": ([vp, vp, sz, sz, optp, u32p], ctypes.c_int),
         "msm_compute_shared": ([vp, vp, sz, sz, optp, u32p], ctypes.c_int),
         "msm_compute_cpu": ([vp, vp, sz, ctypes.c_uint32, ctypes.c_int, u32p], ctypes.c_int),
+        "msm_compute_cocompute": ([vp, vp, sz, optp, ctypes.c_double, ctypes.c_int, u32p], ctypes.c_int),
         "msm_combine_partials": ([vp, sz, u32p], ctypes.c_int),
         "msm_combine_partials_many": ([vp, sz, sz, u32p], ctypes.c_int),
         "msm_point_add_affine": ([u32p, u32p, u32p], ctypes.c_int),
@@ -264,25 +265,34 @@ def get_best_window_size(n: int) -> int:
 
 def compute_msm_wire(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
                      run_length: Optional[int] = None, device: int = -1,
-                     devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
-    """msm_compute on host wire arrays; `devices` shards the points over those HIP ordinals."""
+                     devices: Optional[Sequence[int]] = None, cpu_work_ratio: float = 0.0,
+                     cpu_threads: int = 0) -> Tuple[int, int]:
+    """msm_compute on host wire arrays; `devices` shards the points over those HIP ordinals.
+    cpu_work_ratio > 0 is the reference's CPU/GPU co-compute (?cpuWorkRatio, submission.ts:94-154):
+    the first floor(ratio n) points on the host Pippenger (cpu_threads threads, 0 = all) beside the
+    GPU share, joined with one EC add (msm_compute_cocompute)."""
     L = load()
     pts = _u32(points_wire).reshape(-1, 32)
     sc = _u32(scalars_wire).reshape(-1, 8)
     n = min(pts.shape[0], sc.shape[0])  # the oracle zips to the shorter length
     pts, sc = np.ascontiguousarray(pts[:n]), np.ascontiguousarray(sc[:n])
     o, op = _out(16)
-    _check(L.msm_compute(_ptr(pts), _ptr(sc), n, _opts(window_size, run_length, device, devices=devices), op),
-           "msm_compute")
+    opts = _opts(window_size, run_length, device, devices=devices)
+    if cpu_work_ratio:
+        _check(L.msm_compute_cocompute(_ptr(pts), _ptr(sc), n, opts, float(cpu_work_ratio), int(cpu_threads), op),
+               "msm_compute_cocompute")
+    else:
+        _check(L.msm_compute(_ptr(pts), _ptr(sc), n, opts, op), "msm_compute")
     return _xy(o)
 
 
 def compute_msm(base_affine_points, scalars, window_size: Optional[int] = None,
                 run_length: Optional[int] = None, device: int = -1,
-                devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
-    """compute_msm (submission.ts:25-157): MSM of BigIntPoint[]/U32ArrayPoint[] with bigint[]/Uint32Array[]."""
+                devices: Optional[Sequence[int]] = None, cpu_work_ratio: float = 0.0) -> Tuple[int, int]:
+    """compute_msm (submission.ts:25-157): MSM of BigIntPoint[]/U32ArrayPoint[] with bigint[]/Uint32Array[];
+    cpu_work_ratio as the reference's ?cpuWorkRatio (compute_msm_wire)."""
     return compute_msm_wire(points_to_wire(base_affine_points), scalars_to_wire(scalars), window_size,
-                            run_length, device, devices)
+                            run_length, device, devices, cpu_work_ratio)
 
 
 def compute_msm_partial(points_wire: np.ndarray, scalars_wire: np.ndarray, window_size: Optional[int] = None,
