@@ -136,7 +136,7 @@ int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n,
 
 /* compute_msm with the reference's CPU/GPU co-compute (?cpuWorkRatio, submission.ts:94-154):
  * share = floor(cpu_work_ratio * n) points [0, share) run on the library's host Pippenger
- * (msm_compute_cpu's, cpu_threads threads, <= 0 = all hardware threads, its own window) on a
+ * (msm_compute_cpu's, cpu_threads threads, <= 0 as there, its own window) on a
  * thread of their own while points [share, n) run as msm_compute(opts) on the GPU(s); the two
  * results join with one EC add (point_add_affine, lib.rs:240-253).  cpu_work_ratio 0 (or a share
  * that floors to 0) is msm_compute; a share >= n is the reference's CPU-only branch.  Still a device
@@ -206,7 +206,7 @@ int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars
 /* The reference's CPU-only path (cpuWorkRatio = 1: submission.ts:96-115 -> msm_end_to_end,
  * lib.rs:24-44, 106-121) as the library's own multithreaded host Pippenger: signed c-bit digits,
  * 7M mixed adds into per-thread bucket tables.  window_bits 0 = auto, n_threads <= 0 = all
- * hardware threads.  An explicit entry, never a fallback for the GPU entries. */
+ * hardware threads the process may run (capped by a cgroup CPU quota).  An explicit entry, never a fallback for the GPU entries. */
 int msm_compute_cpu(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, uint32_t window_bits,
                     int n_threads, uint32_t out_xy_be[16]);
 

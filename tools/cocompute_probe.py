@@ -5,7 +5,8 @@ submission.ts:94-154) from host arrays at 2^20 points, per ratio: the evidence b
     python tools/cocompute_probe.py [--n 1048576] [--ratios 0,0.0005,0.001,0.005,0.02] [--runs 5]
 
 One JSON line per ratio: median / min wall ms over the runs (after one warm-up), the host share's
-point count, and whether the result equals the ratio-0 result."""
+point count, whether the result equals the ratio-0 result, and the GPU share alone (msm_compute
+on points [share, n): what the split costs without the host thread)."""
 import argparse
 import json
 import os
@@ -36,8 +37,15 @@ def main():
             res = M.compute_msm_wire(pts, sc, cpu_work_ratio=r, cpu_threads=a.threads)
             ts.append((time.perf_counter() - t0) * 1e3)
             ok = ok and res == ref
-        print(json.dumps({"n": a.n, "cpu_work_ratio": r, "cpu_points": int(r * a.n), "cpu_threads": a.threads,
+        share = int(r * a.n)
+        gs = []
+        for _ in range(a.runs if share else 0):
+            t0 = time.perf_counter()
+            M.compute_msm_wire(pts[share:], sc[share:])
+            gs.append((time.perf_counter() - t0) * 1e3)
+        print(json.dumps({"n": a.n, "cpu_work_ratio": r, "cpu_points": share, "cpu_threads": a.threads,
                           "median_ms": round(statistics.median(ts), 3), "min_ms": round(min(ts), 3),
+                          "gpu_share_alone_median_ms": round(statistics.median(gs), 3) if gs else None,
                           "correct": ok}), flush=True)
 
 

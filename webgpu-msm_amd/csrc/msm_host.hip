@@ -1799,8 +1799,16 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
     for (size_t g = 0; g < G; g++) dsc[g] = base + g * s * 8;
     in.dev_scalars = dsc.data();
   }
+  // The slices' window: that of a 2^17 slice (c = 15) whatever their length.  n not a multiple of
+  // 2^18 makes slices a little short of 2^17 (2^20 - 524 points: 131,007), where pipelined_window
+  // would pick c = 14 -- two more windows' sort and accumulation for a 2% shorter slice
+  // (msm_compute 4.3-4.4 against 3.7 ms; tools/e2e_align_probe.py).
+  msm_opts oc;
+  memset(&oc, 0, sizeof(oc));
+  if (o) oc = *o;
+  if (!oc.window_bits) oc.window_bits = pipelined_window(std::max(s, host_piece()));
   std::vector<Pt> part(G, pt_identity());
-  int rc = run_many(c, in, s, G, o, nullptr, nullptr, true, part.data());
+  int rc = run_many(c, in, s, G, &oc, nullptr, nullptr, true, part.data());
   if (rc != MSM_OK) {
     hipStreamSynchronize(c->copy_stream);  // the scalar copy reads the caller's array
     return rc;
