@@ -339,7 +339,9 @@ uint32_t ilog2(uint32_t v) {
 // re-check with the current launch plan, profiles/r2ab_window_ab.jsonl): c = 14 at 2^16, 15 at
 // 2^17..2^18, 16 from 2^19 (2^19: 0.584-0.592 vs 0.604-0.614 ms at c = 15).
 uint32_t pipelined_window(size_t n) {
-  if (n >= (1u << 19)) return 16;
+  // c = 16 from 7/8 of 2^19: 2^19 - 1 points ran 0.571-0.576 ms at c = 16 against 0.619-0.621 at
+  // c = 15, 3/4 of 2^19 0.451-0.454 at c = 15 against 0.457-0.469 (tools/window_boundary_probe.sh)
+  if (n >= (7u << 16)) return 16;
   if (n >= (1u << 17)) return 15;
   if (n >= (1u << 15)) return 14;
   return msm_best_window(n);
