@@ -125,7 +125,7 @@ uint32_t msm_best_window(size_t n);
 
 /* compute_msm: host-resident inputs, result on the host.  n = 0 gives the identity (0, 1),
  * like the oracle's empty `Address.msm`.  Uploads overlap compute (generalises the reference's
- * staging ring, gpu.ts:146-155 / 244-271): from n = 2^18 the MSM runs as point slices of >= 2^17
+ * staging ring, gpu.ts:146-155 / 244-271): from n = 3 * 2^17 the MSM runs as point slices of ~2^17
  * through the pipelined launches, slice g+1 uploading on a copy stream while slice g computes,
  * and the slices' partials are joined (the shard/join identity of submission.ts:116-154);
  * smaller MSMs upload the scalars first (the bucket sort starts on them) and the points in 8 MiB

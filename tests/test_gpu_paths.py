@@ -36,9 +36,9 @@ def test_host_entry_ragged_pieces():
     assert M.compute_msm_wire(pts[:n2], sc[:n2]) == closed_form(5, 3, sc[:n2])
 
 
-@pytest.mark.parametrize("n", [2 * (1 << 17), 3 * (1 << 17) + 2, (1 << 19) + 7])
+@pytest.mark.parametrize("n", [2 * (1 << 17), 3 * (1 << 17), 3 * (1 << 17) + 2, (1 << 19) + 7])
 def test_host_entry_split_into_slices(n):
-    # msm_compute from host arrays at n >= 2^18 runs G point-slices through the pipelined entry
+    # (2^18: the one-launch path, just below the split) msm_compute from host arrays at n >= 3 x 2^17 runs G point-slices through the pipelined entry
     # (slice g+1 uploads while slice g computes) and joins the partials; n not a multiple of G
     # leaves the last slice short, padded on the device (identity points, zero scalars)
     pts = M.gen_points(n, k0=3, step=5)

@@ -1825,7 +1825,9 @@ int host_entry(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, 
   if ((!points_be || !scalars_be) && n) return MSM_ERR_INVALID_ARG;
   static const bool split_off = getenv("MSM_HOST_SPLIT") && atoi(getenv("MSM_HOST_SPLIT")) == 0;
   return on_device(opts, [&](DevCtx* c) {
-    if (!split_off && n >= 2 * host_piece())
+    // the split from 3 slices' worth: at 2^18 and 2.5 x 2^17 points one launch with its points in
+    // 8 MiB pieces measured 5-10% faster, from 3 x 2^17 the split (tools/e2e_size_probe.py)
+    if (!split_off && n >= 3 * host_piece())
       return run_host_split(c, points_be, scalars_be, n, opts, r);
     return run_host(c, points_be, scalars_be, n, opts, r);
   });
