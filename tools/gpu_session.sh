@@ -43,7 +43,8 @@
 #   lat:VAR=A,B[:R]  single-MSM latency (tools/latency_probe.py) over values of one knob
 #   latlib:LIBS[:R]  single-MSM latency over in-tree library variants
 #   latk:K1,K2[:R]   single-MSM latency over accumulation run lengths
-#   set:VAR=VAL / unset:VAR  environment for the steps that follow (e.g. set:MSM_RED_L=8 kstats1)
+#   set:VAR=VAL / unset:VAR  environment for the steps that follow (e.g. set:MSM_RED_L=8 kstats1;
+#                set:KS=_x suffixes the output names of the steps after it, so repeated steps do not collide)
 #   ubench       the field-multiply and ISA-rate microbenchmarks (tools/ubench)
 #   ldshist      the sort's LDS counting atomics under random, bank-spread and equal keys
 set -u
@@ -161,7 +162,7 @@ for step in "$@"; do
       for r in $(seq 1 "${rounds:-2}"); do
         for v in ${vals//,/ }; do
           export "$var=$v"
-          run "e2eenv_${var}_${v}_$r" 120 python tools/e2e_probe.py --runs 12
+          run "e2eenv_${var}_${v}${KS:-}_$r" 120 python tools/e2e_probe.py --runs 12
           unset "$var"
         done
       done ;;
@@ -190,7 +191,7 @@ for step in "$@"; do
       for r in $(seq 1 "${rounds:-3}"); do
         for v in ${vals//,/ }; do
           export "$var=$v"
-          run "env_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          run "env_${var}_${v}${KS:-}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
           unset "$var"
         done
       done ;;
@@ -200,7 +201,7 @@ for step in "$@"; do
       for r in $(seq 1 "${rounds:-2}"); do
         for v in ${vals//,/ }; do
           export "$var=$v"
-          run "envsize${lg}_${var}_${v}_$r" 180 python bench.py --steps 40 --warmup 10 --no-extras "${BENCH_Q[@]}" \
+          run "envsize${lg}_${var}_${v}${KS:-}_$r" 180 python bench.py --steps 40 --warmup 10 --no-extras "${BENCH_Q[@]}" \
             --n $((1 << lg))
           unset "$var"
         done
