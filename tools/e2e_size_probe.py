@@ -23,20 +23,21 @@ def main():
     ap.add_argument("--sizes", required=True)
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--windows", default="0", help="window widths to time each size at (0 = the library's choice)")
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
     pts = M.gen_points(max(sizes))
     sc = M.gen_scalars(max(sizes), seed=3)
     for r in range(a.rounds):
-        for n in sizes:
+        for n, w in ((n, int(w)) for n in sizes for w in a.windows.split(",")):
             p, s = pts[:n], sc[:n]
-            ok = M.compute_msm_wire(p, s) == closed_form(1, 1, s)
+            ok = M.compute_msm_wire(p, s, window_size=w or None) == closed_form(1, 1, s)
             ts = []
             for _ in range(a.runs):
                 t0 = time.perf_counter()
-                M.compute_msm_wire(p, s)
+                M.compute_msm_wire(p, s, window_size=w or None)
                 ts.append((time.perf_counter() - t0) * 1e3)
-            print(json.dumps({"n": n, "round": r + 1, "median_ms": round(statistics.median(ts), 3),
+            print(json.dumps({"n": n, "window": w, "round": r + 1, "median_ms": round(statistics.median(ts), 3),
                               "min_ms": round(min(ts), 3), "ns_per_point": round(statistics.median(ts) * 1e6 / n, 2),
                               "correct": ok}), flush=True)
 
