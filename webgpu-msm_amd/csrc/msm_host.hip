@@ -1736,7 +1736,7 @@ uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
   return (uint32_t)std::min(std::max(env, 1), (int)MSM_MAX_BATCH);
 }
 
-// One large MSM of host-resident inputs as G point-slices (G <= 16, slices of >= 2^17 points):
+// One large MSM of host-resident inputs as G point-slices (G <= 16, slices of ~2^17 points):
 // MSM = sum_g MSM(slice g), the reference's own shard/join identity (submission.ts:116-154,
 // lib.rs:240-253) inside one GPU.  The slices go through the pipelined entry: slice g+1 uploads
 // on the copy stream while slice g runs, so the PCIe transfer -- the bulk of a host-input MSM --
