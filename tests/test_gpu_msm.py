@@ -430,3 +430,19 @@ def test_reference_format_test_case(tmp_path):
     TD.write_test_case(pp, sp, quads, ss)
     pts, sc = TD.load_test_case(pp, sp)
     assert M.compute_msm_wire(pts, sc) == O.closed_form_msm(ks, ss)
+
+
+def test_many_device_just_past_2p20():
+    """Pipelined launches of two MSMs of 2^20 + 3 points (two per launch up to 2^21)."""
+    torch = pytest.importorskip("torch")
+    import msm_amd as M
+    from _closed_form import closed_form
+
+    n = (1 << 20) + 3
+    d_pts = torch.from_numpy(M.gen_points(n, k0=2, step=3).view(np.int32)).cuda()
+    scs = [M.gen_scalars(n, seed=900 + j) for j in range(3)]
+    d_scs = [torch.from_numpy(s.view(np.int32)).cuda() for s in scs]
+    torch.cuda.synchronize()
+    out = M.compute_msm_many_device([d_pts] * 3, d_scs, n)
+    for r, s in zip(out, scs):
+        assert (O.be_words_to_int(r[:8]), O.be_words_to_int(r[8:])) == closed_form(2, 3, s)

@@ -1413,11 +1413,13 @@ int pipeline_slots(size_t n, const msm_opts* o) {
 // time and an eight-MSM one ~1.04 (profiles/r3/batch_sizes.txt: 0.13 against 0.16 ms per MSM over
 // 50 MSMs, the last launch padded; 2^17 and 2^18 are 2-13% slower with eight), so eight is taken
 // whenever its launches, padded last one included, cost less: ceil(count/8) * 13 < ceil(count/4) * 8.
-// MSM_BATCH overrides (1..MSM_MAX_BATCH).
+// Two also above 2^20, up to 2^21: 2^21 measured 2.31-2.33 ms per MSM with two against 2.36-2.43
+// with one, and one extra point past 2^20 cost 17% with one per launch
+// (1.194 against 1.023 ms, profiles/r4/pipelined_sizes.jsonl).  MSM_BATCH overrides (1..MSM_MAX_BATCH).
 uint32_t pipeline_batch(size_t n, size_t count) {
   static const int env = getenv("MSM_BATCH") ? atoi(getenv("MSM_BATCH")) : 0;
   uint32_t nm = env >= 1 ? (uint32_t)std::min(env, (int)MSM_MAX_BATCH)
-                         : (n <= (1u << 18) ? 4u : n <= (1u << 20) ? 2u : 1u);
+                         : (n <= (1u << 18) ? 4u : n <= (1u << 21) ? 2u : 1u);
   if (env < 1 && n <= (1u << 16) && count >= 8 && (count + 7) / 8 * 13 < (count + 3) / 4 * 8) nm = 8;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
