@@ -84,8 +84,12 @@ typedef struct msm_opts {
  * The ranges of a partition of [0, msm_window_count(c)) sum (as group elements) to the whole MSM,
  * so the window ranges are a second way to shard one MSM over devices besides the point vector:
  * every device then reads all n points and scalars but does 1/D of the bucket work and of the
- * reduction.  Meant for the *_partial entries; window_bits 0, an empty range or one
- * past the last window give MSM_ERR_INVALID_ARG.
+ * reduction.  Meant for the *_partial entries (the affine entries return the
+ * range's sum in affine form, which joins by msm_point_add_affine); window_bits 0, an empty range
+ * or one past the last window give MSM_ERR_INVALID_ARG, and so does the flag on
+ * msm_compute_cocompute (its host share always covers every window).
+ * msm_profile_t.windows reports the launch's range (its window count), not the MSM's layout:
+ * msm_window_count(window_bits) gives that.
  * With MSM_FLAG_HALF_WINDOWS the range is counted in half windows, [0, 2 msm_window_count(c)):
  * half window 2w is window w's buckets of the lower half of its digit magnitudes, 2w + 1 the upper
  * half, so a range may start or end in the middle of a window (an odd number of windows can be

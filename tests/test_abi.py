@@ -2,6 +2,7 @@
 libmsm.so, and the host-side entry points (split, point_add_affine, combine, generators) agree
 with the oracle."""
 import ctypes
+import json
 import os
 import re
 import shutil
@@ -54,6 +55,37 @@ def test_addon_exports():
                                           "bestWindowSize", "init", "deviceCount", "deviceOrdinals", "strerror"])
 
 
+def test_addon_bigint_marshalling_errors():
+    """computeMsmBigInt checks every coordinate while marshalling (in blocks of 1,024 points, each
+    in its own handle scope): a bad element past the first block is still reported synchronously
+    with the reference's error class, and a throwing getter's own exception propagates."""
+    node = shutil.which("node")
+    if not node:
+        pytest.skip("node not installed")
+    addon = os.path.join(ROOT, "webgpu-msm_amd", "js", "msm_napi.node")
+    script = f"""
+const a = require({addon!r});
+const n = 3000;
+const pts = Array.from({{length: n}}, () => ({{x: 1n, y: 2n, t: 3n, z: 1n}}));
+const sc = Array.from({{length: n}}, () => 5n);
+const out = [];
+const tryit = (f) => {{ try {{ f(); return 'ok'; }} catch (e) {{ return e.constructor.name + ':' + e.message; }} }};
+const p1 = pts.slice(); p1[2500] = {{x: -1n, y: 2n, t: 3n, z: 1n}};
+out.push(tryit(() => a.computeMsmBigInt(p1, sc)));
+const s1 = sc.slice(); s1[1500] = 1n << 256n;
+out.push(tryit(() => a.computeMsmBigInt(pts, s1)));
+const p2 = pts.slice(); p2[2048] = {{get x() {{ throw new Error('getter'); }}, y: 2n, t: 3n, z: 1n}};
+out.push(tryit(() => a.computeMsmBigInt(p2, sc)));
+out.push(tryit(() => a.computeMsmBigInt(5, sc)));
+console.log(JSON.stringify(out));
+"""
+    got = json.loads(subprocess.run([node, "-e", script], capture_output=True, text=True, check=True).stdout)
+    assert got[0] == "RangeError:point coordinate must be a bigint in [0, 2^256)"
+    assert got[1] == "RangeError:scalar must be a bigint in [0, 2^256)"
+    assert got[2] == "Error:getter"
+    assert got[3].startswith("TypeError:")
+
+
 def test_init_reports_device_state():
     rc = M.load().msm_init()
     assert rc in (0, -6)
@@ -73,6 +105,19 @@ def test_cocompute_rejects_bad_ratio(ratio):
     with pytest.raises(M.MsmError) as e:
         M.compute_msm_wire(O.gen_points(3), O.ints_to_be_words([1, 2, 3]), cpu_work_ratio=ratio)
     assert e.value.code == -1
+
+
+@pytest.mark.parametrize("ratio", [0.0, 0.5, 1.0])
+def test_cocompute_rejects_window_range(ratio):
+    """A window range (MSM_FLAG_WINDOWS) has no host counterpart: msm_compute_cocompute rejects it
+    before touching a device, at every ratio."""
+    L = M.load()
+    pts, sc = O.gen_points(3), O.ints_to_be_words([1, 2, 3])
+    o = np.zeros(16, np.uint32)
+    opts = M._opts(15, windows=(0, 8))
+    rc = L.msm_compute_cocompute(M._ptr(np.ascontiguousarray(pts, np.uint32)), M._ptr(np.ascontiguousarray(sc, np.uint32)),
+                                 3, opts, float(ratio), 1, o.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    assert rc == -1
 
 
 def test_strerror_and_best_window():

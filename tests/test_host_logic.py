@@ -282,3 +282,52 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode != 0
     assert "gfx950 device(s) visible" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def _top_window_bucket_bound(n, c):
+    """lambda + 5 sqrt(lambda) + 2 of the largest expected bucket of an n-point MSM at window width c
+    (uniform scalars mod p; the top main window's digits stop at p >> offset), from the Python
+    window layout, independently of libmsm's run_length_skew_floor."""
+    import math
+
+    wm = -(-254 // c)
+    q, nhi = 254 // wm, 254 - (254 // wm) * wm
+    lam = 0.0
+    for w in range(wm):
+        b = q + 1 if w < nhi else q
+        vals = 1 << (b - 1)
+        if w == wm - 1:
+            off = w * q + min(w, nhi)
+            vals = min(vals, (O.P >> off) + 1)
+        lam = max(lam, n / vals)
+    return lam + 5 * math.sqrt(lam) + 2
+
+
+@pytest.mark.parametrize("n,nm,pipelined", [(1 << 20, 2, True), ((1 << 20) + 1, 2, True), (1 << 20, 1, False),
+                                            ((1 << 20) + 1, 1, False), (1 << 21, 2, True), (1 << 21, 1, False),
+                                            (5 << 18, 2, True), (3 << 18, 2, True), (1 << 18, 4, True),
+                                            (1 << 17, 4, True), (1 << 16, 8, True), (1 << 19, 1, False),
+                                            (4096, 1, False), (1000, 1, False)])
+def test_run_length_clears_the_skew_joins(n, nm, pipelined):
+    """The plan's run length K keeps every expected bucket under three whole runs (3 K + 2 entries:
+    the skew joins' trigger in k_accumulate), so random scalars never take the second reduction;
+    K is a multiple of 4 (16-B entry loads)."""
+    pl = M.launch_plan(n, nm, pipelined)
+    K = pl["run_length"]
+    assert K % 4 == 0 and 16 <= K <= 4096
+    assert 3 * K + 2 > _top_window_bucket_bound(n, pl["c"])
+    assert K >= pl["skew_floor"]
+
+
+def test_run_length_past_a_power_of_two():
+    """The round-4 cliff: one point past 2^20 no longer shortens K (2^20 + 1 was 14% slower than
+    2^20 at K = 44, the skew joins on every launch).  Pipelined launches keep K = 64; a lone MSM
+    takes one round of K = 68 instead of two rounds; 2^20 itself and the small four-MSM launches
+    (one round filled by a shorter K) are unchanged."""
+    assert M.launch_plan(1 << 20, 2, True)["run_length"] == 64
+    assert M.launch_plan((1 << 20) + 1, 2, True)["run_length"] == 64
+    assert M.launch_plan(1 << 20, 1, False)["run_length"] == 64
+    assert M.launch_plan((1 << 20) + 1, 1, False)["run_length"] == 68
+    assert M.launch_plan(1 << 17, 4, True)["run_length"] == 36
+    # an explicit run length is taken as given
+    assert M.launch_plan((1 << 20) + 1, 2, True, run_length=44)["run_length"] == 44

@@ -230,6 +230,42 @@ for step in "$@"; do
           run "latk_${k}_$r" 120 python tools/latency_probe.py --run-length "$k"
         done
       done ;;
+    calltrace:*)  # calltrace:K -- kernel trace of the 2^20 bench at K timed steps; fill / drain of the timed call
+      IFS=: read -r _ k <<< "$step"
+      # shellcheck disable=SC2086
+      run "calltrace${k}${KS:-}" 300 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/${TAG}_calltrace${k}${KS:-}_d" \
+        -o run -- python3 bench.py --steps "$k" --warmup 5 --no-extras "${BENCH_Q[@]}" ${BENCH_X:-}
+      tr=$(find "gpurun_out/${TAG}_calltrace${k}${KS:-}_d" -name '*kernel_trace.csv' | head -1)
+      run "calltrace${k}${KS:-}_tl" 60 python tools/call_timeline.py "$tr" --launches $(( (k + 1) / 2 )) ;;
+    rl:*)  # rl:N:K1,K2[:R] -- pipelined ms per MSM at N points over accumulation run lengths (0 = the plan's)
+      IFS=: read -r _ nn ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "rl${nn}_k${k}_$r" 120 python bench.py --steps 20 --warmup 5 --no-extras "${BENCH_Q[@]}" --n "$nn" \
+            --run-length "$k"
+        done
+      done ;;
+    warm:*)  # warm:K:W1,W2[:R] -- the 2^20 bench at K timed steps over --warm-s values (clock ramp)
+      IFS=: read -r _ k ws rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for w in ${ws//,/ }; do
+          run "warm${k}_w${w}_$r" 120 python bench.py --steps "$k" --warmup 5 --no-extras "${BENCH_Q[@]}" --warm-s "$w"
+        done
+      done ;;
+    batch64rl:*)  # batch64rl:K1,K2[:R] -- the 64 x 2^18 prover batch over run lengths (0 = the plan's)
+      IFS=: read -r _ ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "batch64_k${k}_$r" 180 python bench.py --batch 64 --n 262144 --steps 10 --warmup 3 --run-length "$k"
+        done
+      done ;;
+    latn:*)  # latn:N:K1,K2[:R] -- single-MSM latency at N points over run lengths (0 = the plan's)
+      IFS=: read -r _ nn ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "latn${nn}_k${k}_$r" 120 python tools/latency_probe.py --n "$nn" --run-length "$k"
+        done
+      done ;;
     set:*) export "${step#set:}" ;;
     unset:*) unset "${step#unset:}" ;;
     ubench)

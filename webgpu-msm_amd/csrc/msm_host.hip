@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -372,30 +373,72 @@ uint32_t bucket_reduce_L(const MsmDims& d, const DevShape& sh) {
   return 16;
 }
 
+// The shortest run length that keeps random scalars off the skew joins.  A bucket that holds
+// three whole runs (3 K + 2 entries or more) sends its workgroup to k_chain_join, and the launch
+// through a second reduction (~0.25 ms at 2^20: DESIGN.md §2.4).  The largest buckets are the top
+// main window's: its digits only reach p >> offset (p < 2^253; 9,551 values at c = 16), so at 2^20
+// they hold ~110 entries each, against 32-64 in the other windows.  K is sized for the largest
+// expected bucket of the launch's range, lambda + 5 sqrt(lambda) + 2 entries (Poisson, uniform
+// scalars mod p).  This is what made 2^20 + 1 points 14% slower than 2^20 (round 4): K = 44 there,
+// so a top-window bucket of ~134+ entries (one in ~10^4) held three runs in every launch.
+uint32_t run_length_skew_floor(const MsmDims& d) {
+  double lam_max = 0;
+  for (uint32_t l = 0; l < d.Wr; l++) {
+    const uint32_t w = d.w0 + l;
+    if (w + 1 >= d.Wm) continue;  // the overflow window: empty for canonical scalars
+    double vals = (double)(1u << (win_bits(d, w) - 1));
+    if (w + 2 == d.Wm) {  // the top main window: digits below (p >> off) + 1
+      const uint32_t off = win_off(d, w);
+      const double top = off >= 192 ? (double)(P[3] >> (off - 192)) + 1.0 : vals;
+      vals = std::min(vals, top);
+    }
+    lam_max = std::max(lam_max, (double)d.n / vals);
+  }
+  const double maxb = lam_max + 5.0 * std::sqrt(lam_max) + 2.0;
+  const uint32_t k = (uint32_t)std::floor((maxb - 2.0) / 3.0) + 1;  // 3 K + 2 > maxb
+  return (k + 3) & ~3u;
+}
+
 // Run length K (entries per k_accumulate lane, a multiple of 4 for the 16-B entry loads): the
 // accumulation holds sh.acc_waves waves per SIMD (4: VGPR- and LDS-bound, from the runtime's
-// occupancy query for the device), so its lanes run in rounds of that
-// many x 4 x CUs waves, and a round only partly filled runs on few SIMDs for a full wave's time.
-// So K <= 64 (long enough to amortise the per-run joins) is chosen to fill whole rounds: the
-// fewest rounds r with K <= 64, then the smallest K that fits the launch's entries in r rounds
-// (upper bound: every main-window digit nonzero).  2^20, two MSMs: K = 64, 2 rounds; 2^17, four
-// MSMs: K = 36 (3,868 waves) where K = 32 needed 4,352, a 6% second round.  K also bounds how
-// many runs a bucket spans: a bucket over 3 or more whole runs sends the launch through the skew
-// joins (§2.4 of DESIGN.md), so shorter runs than these cost a second reduction on random
-// scalars (a lone 2^20 MSM at K = 44: latency 1.16 -> 1.36 ms).
-uint32_t run_length_for(const MsmDims& d, const DevShape& sh) {
+// occupancy query for the device), so its lanes run in rounds of that many x 4 x CUs waves.
+// - A launch under one round at K = 64 takes the smallest K that fills the round (2^17, four MSMs:
+//   K = 36, 3,868 waves, where K = 32 needed 4,352: a 6% second round that runs on few SIMDs).
+// - Pipelined launches past one round keep K = 64 (2^20, two MSMs: two whole rounds): the next
+//   launch's kernels fill whatever a short last round leaves idle.  2^20 + 1 points, two MSMs:
+//   1.030 ms per MSM at K = 64 against 1.062 at K = 68 (two rounds) and 1.170 at the balanced
+//   K = 44 (skew joins) (profiles/r5/run_length_2p20p1.jsonl).
+// - A lone MSM past one round (its latency counts, and nothing fills its tail) takes the K up to
+//   128 whose whole rounds cost least (rounds x K): 2^20 + 1 points run one round of K = 68.
+// K never drops below run_length_skew_floor.  (Upper bound of the entries: every main-window
+// digit nonzero.)
+uint32_t run_length_for(const MsmDims& d, const DevShape& sh, bool pipelined) {
   // main windows of the launch's range (the overflow window holds no entry for canonical scalars)
   const uint64_t nmain = d.Wr - ((d.w0 + d.Wr == d.Wm) ? 1u : 0u);
   const uint64_t m = (uint64_t)d.nm * std::max<uint64_t>(1, nmain) * d.n;
   const uint64_t round_lanes =
       64ull * (uint64_t)std::max(1, sh.acc_waves) * 4 * (uint64_t)(sh.n_cu > 0 ? sh.n_cu : 256);
-  const uint64_t r = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
-  uint64_t K = (m + r * round_lanes - 1) / (r * round_lanes);
+  const uint64_t kfloor = std::max<uint64_t>(16, run_length_skew_floor(d));
+  const uint64_t r64 = std::max<uint64_t>(1, (m + 64 * round_lanes - 1) / (64 * round_lanes));
+  uint64_t K;
+  if (r64 == 1) {
+    K = (m + round_lanes - 1) / round_lanes;  // one round
+  } else if (pipelined) {
+    K = 64;
+  } else {
+    uint64_t best = ~0ull;
+    K = 64;
+    for (uint64_t k = 16; k <= 128; k += 4) {
+      if (k < kfloor) continue;
+      const uint64_t cost = (m + k * round_lanes - 1) / (k * round_lanes) * k;
+      if (cost < best) best = cost, K = k;
+    }
+  }
   K = (K + 3) & ~3ull;
-  return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, K));
+  return (uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(kfloor, K));
 }
 
-int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl);
+int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl, bool pipelined = false);
 
 int make_plan(size_t n, const msm_opts* o, const DevShape& sh, Plan* pl, bool pipelined = false, uint32_t nm = 1,
               bool shared = false) {
@@ -442,14 +485,14 @@ int make_plan(size_t n, const msm_opts* o, const DevShape& sh, Plan* pl, bool pi
   d.nbins = d.W * d.nbc;
   d.ch = PT_THREADS * PS_R;  // 16384 digits per partition chunk (>= 64 per bin slice while nbc <= 256)
   d.nch = (uint32_t)((n + d.ch - 1) / d.ch);
-  return finish_plan(d, o, sh, pl);
+  return finish_plan(d, o, sh, pl, pipelined);
 }
 
 // The launch-shape fields that follow from the geometry d.
-int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl) {
+int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* pl, bool pipelined) {
   const size_t n = d.n;
   pl->d = d;
-  pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, sh);
+  pl->K = (o && o->run_length) ? o->run_length : run_length_for(d, sh, pipelined);
   if (pl->K < 1 || pl->K > 4096) return MSM_ERR_INVALID_ARG;
   pl->L = bucket_reduce_L(d, sh);
   pl->nchunks = (d.B + pl->L - 1) / pl->L;
@@ -1807,9 +1850,24 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   // 2^18 makes slices a little short of 2^17 (2^20 - 524 points: 131,007), where pipelined_window
   // would pick c = 14 -- two more windows' sort and accumulation for a 2% shorter slice
   // (msm_compute 4.3-4.4 against 3.7 ms; tools/e2e_align_probe.py).
+  // field by field: a caller built against the original 16-byte msm_opts owns no fields past
+  // `flags`, and the later ones are read only under the flags that announce them (msm.h)
   msm_opts oc;
   memset(&oc, 0, sizeof(oc));
-  if (o) oc = *o;
+  if (o) {
+    oc.window_bits = o->window_bits;
+    oc.run_length = o->run_length;
+    oc.device = o->device;
+    oc.flags = o->flags;
+    if (o->flags & MSM_FLAG_DEVICES) {
+      oc.devices = o->devices;
+      oc.n_devices = o->n_devices;
+    }
+    if (o->flags & MSM_FLAG_WINDOWS) {
+      oc.window_lo = o->window_lo;
+      oc.window_hi = o->window_hi;
+    }
+  }
   if (!oc.window_bits) oc.window_bits = pipelined_window(std::max(s, host_piece()));
   std::vector<Pt> part(G, pt_identity());
   int rc = run_many(c, in, s, G, &oc, nullptr, nullptr, true, part.data());
@@ -2162,6 +2220,9 @@ int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n,
 int msm_compute_cocompute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                           double cpu_work_ratio, int cpu_threads, uint32_t out_xy_be[16]) {
   if (!out_xy_be || ((!points_be || !scalars_be) && n) || !(cpu_work_ratio >= 0.0)) return MSM_ERR_INVALID_ARG;
+  // a window range has no CPU counterpart (the host Pippenger computes every window): joining a
+  // range's GPU share with a whole CPU share would be silently wrong
+  if (opts && (opts->flags & MSM_FLAG_WINDOWS)) return MSM_ERR_INVALID_ARG;
   // cpuShare = floor(cpuWorkRatio * n) (submission.ts:98); >= n is the reference's CPU-only branch
   const double share_d = cpu_work_ratio * (double)n;
   const size_t share = share_d >= (double)n ? n : (size_t)share_d;
@@ -2531,6 +2592,19 @@ int msm_test_tail_batch(size_t n, uint32_t k, const uint32_t* terms, int helpers
   }
   *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   for (uint32_t m = 0; m < k; m++) pt_to_be_affine(r[m], out_xy_be + 16 * m);
+  return MSM_OK;
+}
+
+// The launch plan make_plan builds for n points, nm MSMs per launch, pipelined or lone, with
+// `opts` (window width / range; may be null): out = {c (widest window), windows in the launch per
+// MSM (Wr), run length K, reduction chunk L, MSMs per launch, coarse bins per window, skew floor
+// of K}, for the default device shape (256 CUs, 4 accumulation waves per SIMD).
+int msm_test_plan(size_t n, uint32_t nm, int pipelined, const msm_opts* opts, uint32_t out[7]) {
+  if (!out || nm < 1 || nm > MSM_MAX_BATCH) return MSM_ERR_INVALID_ARG;
+  Plan pl;
+  if (int rc = make_plan(n, opts, DevShape{}, &pl, pipelined != 0, nm)) return rc;
+  const uint32_t v[7] = {pl.d.c, pl.d.Wr, pl.K, pl.L, pl.d.nm, pl.d.nbc, run_length_skew_floor(pl.d)};
+  memcpy(out, v, sizeof(v));
   return MSM_OK;
 }
 

@@ -297,27 +297,50 @@ napi_value ComputeMsmBigInt(napi_env env, napi_callback_info info) {
   j->n = std::min(np_, ns);
   j->points.resize(j->n * 32);
   j->scalars.resize(j->n * 8);
-  static const char* keys[4] = {"x", "y", "t", "z"};
-  for (uint32_t i = 0; i < j->n; i++) {
-    napi_value p, s;
-    if (napi_get_element(env, argv[0], i, &p) != napi_ok || napi_get_element(env, argv[1], i, &s) != napi_ok) {
+  // The four property keys are made once per call (napi_get_named_property would create and
+  // intern a string per coordinate: 4 n of them), and the element handles live in one handle
+  // scope per block of points, so the handle stack stays small instead of growing by ~6 n handles.
+  static const char* names[4] = {"x", "y", "t", "z"};
+  napi_value keys[4];
+  for (int k = 0; k < 4; k++)
+    if (napi_create_string_utf8(env, names[k], 1, &keys[k]) != napi_ok) {
       delete j;
-      napi_throw_error(env, nullptr, "bad input element");
+      napi_throw_error(env, nullptr, "cannot create the coordinate keys");
       return nullptr;
     }
-    for (int k = 0; k < 4; k++) {
-      napi_value c;
-      if (napi_get_named_property(env, p, keys[k], &c) != napi_ok || !bigint_be(env, c, &j->points[i * 32 + 8 * k])) {
-        delete j;
-        napi_throw_range_error(env, nullptr, "point coordinate must be a bigint in [0, 2^256)");
-        return nullptr;
+  constexpr uint32_t BLOCK = 1024;
+  const char* bad = nullptr;  // the error of the first bad element, thrown after its scope closes
+  for (uint32_t i0 = 0; i0 < j->n && !bad; i0 += BLOCK) {
+    napi_handle_scope scope;
+    if (napi_open_handle_scope(env, &scope) != napi_ok) {
+      bad = "bad input element";
+      break;
+    }
+    const uint32_t i1 = std::min<uint32_t>(j->n, i0 + BLOCK);
+    for (uint32_t i = i0; i < i1 && !bad; i++) {
+      napi_value p, s;
+      if (napi_get_element(env, argv[0], i, &p) != napi_ok || napi_get_element(env, argv[1], i, &s) != napi_ok) {
+        bad = "bad input element";
+        break;
       }
+      for (int k = 0; k < 4 && !bad; k++) {
+        napi_value c;
+        if (napi_get_property(env, p, keys[k], &c) != napi_ok || !bigint_be(env, c, &j->points[i * 32 + 8 * k]))
+          bad = "point coordinate must be a bigint in [0, 2^256)";
+      }
+      if (!bad && !bigint_be(env, s, &j->scalars[i * 8])) bad = "scalar must be a bigint in [0, 2^256)";
     }
-    if (!bigint_be(env, s, &j->scalars[i * 8])) {
-      delete j;
-      napi_throw_range_error(env, nullptr, "scalar must be a bigint in [0, 2^256)");
-      return nullptr;
+    napi_close_handle_scope(env, scope);
+  }
+  if (bad) {
+    delete j;
+    bool pending = false;
+    napi_is_exception_pending(env, &pending);  // a throwing getter: keep its exception
+    if (!pending) {
+      if (bad[0] == 'b') napi_throw_error(env, nullptr, bad);
+      else napi_throw_range_error(env, nullptr, bad);
     }
+    return nullptr;
   }
   j->window = argc > 2 ? get_window(env, argv[2]) : 0;
   return start_job(env, j);

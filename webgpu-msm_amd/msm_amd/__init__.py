@@ -134,6 +134,7 @@ def load() -> ctypes.CDLL:
                               u32p], ctypes.c_int),
         "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_tail_words": ([sz], sz),
+        "msm_test_plan": ([sz, ctypes.c_uint32, ctypes.c_int, optp, u32p], ctypes.c_int),
         "msm_test_tail_batch": ([sz, ctypes.c_uint32, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_peer_state": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -308,6 +309,18 @@ def compute_msm_partial(points_wire: np.ndarray, scalars_wire: np.ndarray, windo
                                  _opts(window_size, None, device, devices=devices, windows=windows), op),
            "msm_compute_partial")
     return o
+
+
+def launch_plan(n: int, nm: int = 1, pipelined: bool = False, window_size: Optional[int] = None,
+                run_length: Optional[int] = None, windows: Optional[Tuple[int, int]] = None) -> dict:
+    """The launch plan libmsm builds for n points and nm MSMs per launch (msm_test_plan; default
+    device shape): window width c, windows per MSM in the launch, run length K, reduction chunk L,
+    coarse bins per window and the skew floor of K.  No GPU needed."""
+    out = np.zeros(7, np.uint32)
+    _check(load().msm_test_plan(n, nm, int(pipelined), _opts(window_size, run_length, windows=windows),
+                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))), "msm_test_plan")
+    return dict(zip(("c", "windows", "run_length", "chunk_len", "msms_per_launch", "coarse_bins", "skew_floor"),
+                    (int(v) for v in out)))
 
 
 def window_count(window_size: int) -> int:
