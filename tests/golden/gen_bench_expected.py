@@ -5,7 +5,8 @@ Inputs follow the survey's spec: P_i = (i+1) G with G the bench
 (AllBenchmarks.tsx:111-119), scalars from xorshift64(13,7,17) seeded XORSHIFT_SEED + j, 4 words
 each (first most significant), reduced mod p.  Expected value = ((sum s_i (i+1)) mod r) G, the
 closed form the survey verified against the Aleo-wasm oracle at 2^12, 2^16 and 2^20 (seed j = 0;
-this script re-asserts those rows).
+this script re-asserts those rows).  Rows "d<n>:<j>" hold the distinct-base prover batch: MSM j over
+P_i = (j n + i + 1) G with seed XORSHIFT_SEED + j.
 
     python tests/golden/gen_bench_expected.py        (~1 min, pure Python)
 """
@@ -22,13 +23,16 @@ from oracle import oracle as O  # noqa: E402
 ROWS = [(1 << lg, j) for lg in (16, 17, 18, 19, 20) for j in range(4)]
 ROWS += [(1 << 18, j) for j in range(4, 64)]  # the prover batch (BASELINE configs[4]): 64 seeds
 ROWS += [(1 << 16, j) for j in range(4, 64)]  # the same batch shape at 2^16 (quick runs)
+# The prover batch with DISTINCT bases (bench.py --batch 64 --distinct): MSM j of n points runs over
+# P_i = (j n + i + 1) G, i.e. the j-th n-point slice of one long point vector, with scalar seed j.
+DISTINCT = [(1 << 18, j) for j in range(64)] + [(1 << 16, j) for j in range(64)]
 
 
-def expected(n: int, j: int):
+def expected(n: int, j: int, k0: int = 1):
     ss = O.xorshift_scalars(n, O.XORSHIFT_SEED + j)
     acc = 0
     for i, s in enumerate(ss):
-        acc += (i + 1) * s
+        acc += (k0 + i) * s
     return O.scalar_mul(O.G, acc % O.R_ORDER)
 
 
@@ -44,6 +48,10 @@ def main():
             assert (x, y) == survey[n], f"closed form disagrees with the survey-recorded oracle at n={n}"
         out["rows"][f"{n}:{j}"] = [str(x), str(y)]
         print(n, j, flush=True)
+    for n, j in DISTINCT:  # "d<n>:<j>": MSM j over P_i = (j n + i + 1) G
+        x, y = expected(n, j, k0=j * n + 1)
+        out["rows"][f"d{n}:{j}"] = [str(x), str(y)]
+        print("distinct", n, j, flush=True)
     with open(os.path.join(HERE, "bench_expected.json"), "w") as f:
         json.dump(out, f, indent=0)
 

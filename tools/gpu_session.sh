@@ -113,6 +113,7 @@ for step in "$@"; do
         run size${lg}_k20 120 python bench.py --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
       done ;;
     batch64) run batch64 300 python bench.py --batch 64 --n 262144 ;;
+    batch64d) run batch64d 300 python bench.py --batch 64 --n 262144 --distinct ;;  # distinct base vectors
     gloo8)
       MSM_DIST_BACKEND=gloo OMP_NUM_THREADS=2 run gloo8 400 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 2 \
@@ -192,6 +193,16 @@ for step in "$@"; do
         for v in ${vals//,/ }; do
           export "$var=$v"
           run "env_${var}_${v}${KS:-}_$r" 180 python bench.py --steps 40 --warmup 10 "${BENCH_Q[@]}"
+          unset "$var"
+        done
+      done ;;
+    envk:*)  # envk:K:VAR=A,B[:R] -- the 2^20 bench at K timed steps (warm-up 5: the driver's shape) over one knob
+      IFS=: read -r _ k spec rounds <<< "$step"
+      var=${spec%%=*}; vals=${spec#*=}
+      for r in $(seq 1 "${rounds:-3}"); do
+        for v in ${vals//,/ }; do
+          export "$var=$v"
+          run "envk${k}_${var}_${v}${KS:-}_$r" 180 python bench.py --steps "$k" --warmup 5 --no-extras "${BENCH_Q[@]}"
           unset "$var"
         done
       done ;;

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -172,6 +173,7 @@ struct Segment {
   int parts = 0;
   const uint32_t* pts_buf = nullptr;  // the point-record buffer the captured kernels use
   bool acc_events = false;            // event-record nodes around k_accumulate
+  bool fork = false;                  // the preparation forked beside the sort (slot_forks)
   uint64_t gen = 0;
   uint64_t used = 0;
   hipGraph_t graph = nullptr;
@@ -211,11 +213,13 @@ struct Slot {
   hipEvent_t ev_sc = nullptr;  // the scalars of the slot's next launch are in place (host uploads)
   Plan pl{};
   bool acc_timed = false;
+  bool pipelined = false;  // a launch of a pipelined run (another launch in flight beside it)
 };
 constexpr int NSLOT = 4;      // at most this many launches in flight (one HIP stream each)
 constexpr int NCHUNK_EV = 8;  // events marking uploaded point chunks
 
 class TailCrew;
+class HornerPool;
 
 // What the launch plans take from the device: compute units, and k_accumulate's waves per SIMD
 // (the occupancy query at context creation; run_length_for fills whole rounds of them).  The test
@@ -236,6 +240,7 @@ struct DevCtx {
   hipEvent_t ev_shared = nullptr;
   Buf shared_pts;  // point records of a shared base vector (msm_compute_shared*)
   Buf host_sc;     // all the scalars of a split host-input MSM (run_host_split), uploaded first
+  Buf host_pts;    // and all its points, slice by slice (no slot buffer reused within the call)
   hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
   int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate + device total per launch
   // The launch sequence of each slot is captured into HIP graphs and replayed: one
@@ -246,6 +251,10 @@ struct DevCtx {
   std::vector<std::pair<float, float>> acc_ivals;
   msm_profile_t last{};
   TailCrew* crew = nullptr;  // a lone MSM's host-tail helpers (persistent, created on first use)
+  HornerPool* pool = nullptr;  // the pipelined entries' host tails, off the launching thread
+  // per-launch upload events of a host-input pipelined run (launch j: up_ev[2 j] its scalars,
+  // up_ev[2 j + 1] all its inputs), grown on demand
+  std::vector<hipEvent_t> up_ev;
 };
 
 std::mutex g_mu;
@@ -288,10 +297,13 @@ int get_ctx(int device, DevCtx** out) {
       delete c;
       return MSM_ERR_HIP;
     }
+    // Streams in this order because the runtime deals them round-robin over its hardware queues
+    // (GPU_MAX_HW_QUEUES, 4 by default) and two streams on one queue run in order: the slots'
+    // streams first, so the launches in flight never share a queue (three slots for host inputs
+    // beside the copy stream), then the aux streams of the preparation fork.
     bool ok = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
-    for (Slot& sl : c->slot)
-      ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess &&
-           hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking) == hipSuccess;
+    for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
+    for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
       delete c;
       hipSetDevice(prev);
@@ -404,10 +416,11 @@ uint32_t run_length_skew_floor(const MsmDims& d) {
 // occupancy query for the device), so its lanes run in rounds of that many x 4 x CUs waves.
 // - A launch under one round at K = 64 takes the smallest K that fills the round (2^17, four MSMs:
 //   K = 36, 3,868 waves, where K = 32 needed 4,352: a 6% second round that runs on few SIMDs).
-// - Pipelined launches past one round keep K = 64 (2^20, two MSMs: two whole rounds): the next
+// - Pipelined launches past one round take the K of whole rounds (2^20, two MSMs: K = 64, two
+//   rounds) unless that K is under the skew floor: then K = 64 (or the floor), and the next
 //   launch's kernels fill whatever a short last round leaves idle.  2^20 + 1 points, two MSMs:
 //   1.030 ms per MSM at K = 64 against 1.062 at K = 68 (two rounds) and 1.170 at the balanced
-//   K = 44 (skew joins) (profiles/r5/run_length_2p20p1.jsonl).
+//   K = 44 (skew joins) (profiles/r5/run_length.jsonl).
 // - A lone MSM past one round (its latency counts, and nothing fills its tail) takes the K up to
 //   128 whose whole rounds cost least (rounds x K): 2^20 + 1 points run one round of K = 68.
 // K never drops below run_length_skew_floor.  (Upper bound of the entries: every main-window
@@ -424,7 +437,11 @@ uint32_t run_length_for(const MsmDims& d, const DevShape& sh, bool pipelined) {
   if (r64 == 1) {
     K = (m + round_lanes - 1) / round_lanes;  // one round
   } else if (pipelined) {
-    K = 64;
+    // whole rounds of a shorter K where that clears the skew floor (2^18, four MSMs: K = 36,
+    // 0.332-0.337 ms per MSM against 0.340-0.342 at K = 64), else K = 64
+    K = (m + r64 * round_lanes - 1) / (r64 * round_lanes);
+    K = (K + 3) & ~3ull;
+    if (K < kfloor) K = std::max<uint64_t>(64, kfloor);
   } else {
     uint64_t best = ~0ull;
     K = 64;
@@ -569,6 +586,12 @@ bool fork_prepare() {
   static const bool on = !(getenv("MSM_FORK_PREP") && atoi(getenv("MSM_FORK_PREP")) == 0);
   return on;
 }
+// The same for the launches of a pipelined run (MSM_FORK_PREP_PIPE, default on).
+bool fork_prepare_pipelined() {
+  static const bool on = !(getenv("MSM_FORK_PREP_PIPE") && atoi(getenv("MSM_FORK_PREP_PIPE")) == 0);
+  return on;
+}
+bool slot_forks(const Slot& sl) { return sl.pipelined ? fork_prepare() && fork_prepare_pipelined() : fork_prepare(); }
 
 // Whether k_prepare_points writes `records` point records with nontemporal stores: only when they
 // outgrow the Infinity Cache (>= 128 MiB, i.e. 2^20 records; MSM_PP_NT=0/1 forces it).
@@ -607,7 +630,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   // sequence the preparation forks onto the slot's aux stream (a parallel branch of the captured
   // graph) and rejoins before the accumulation, so a lone MSM's sort no longer waits behind it.
   // (Profiling mode 1 keeps them in order, one event between every phase.)
-  const bool fork = (parts & PART_PREP) && (parts & PART_SORT) && !prof && fork_prepare();
+  const bool fork = (parts & PART_PREP) && (parts & PART_SORT) && !prof && slot_forks(sl);
   if (parts & PART_PREP) {
     mark(PH_START);
     hipStream_t ps = s;
@@ -926,6 +949,72 @@ class TailCrew {
   std::unique_ptr<std::atomic<int>[]> ready_, odone_;
 };
 
+// Host tails of a pipelined run's launches (all but the last, whose tails are the run's drain and
+// go over the TailCrew), on persistent worker threads: the launching thread only waits for a
+// launch, copies its terms and enqueues the next one.  With the tails on the launching thread, a
+// slot whose launch finished while that thread was busy with another launch's Horner waited for
+// it: a kernel trace of the 2^20 bench showed one slot's next launch 300 us behind the other's
+// while the device ran only that other's sort (profiles/r5/pipeline_gap.txt).
+class HornerPool {
+ public:
+  explicit HornerPool(int threads) {
+    for (int i = 0; i < threads; i++) th_.emplace_back([this] { work(); });
+  }
+  ~HornerPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  void push(std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(fn));
+      pending_++;
+    }
+    cv_.notify_one();
+  }
+  // every job pushed so far has run
+  void wait_all() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return quit_ || !q_.empty(); });
+        if (q_.empty()) return;  // quit with nothing left
+        fn = std::move(q_.front());
+        q_.pop_front();
+      }
+      fn();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--pending_ == 0) done_cv_.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<std::function<void()>> q_;
+  int pending_ = 0;
+  bool quit_ = false;
+};
+
+// Worker threads of the pool (MSM_HORNER_THREADS; 0 = the launching thread runs the tails itself).
+int horner_threads() {
+  static const int v =
+      getenv("MSM_HORNER_THREADS") ? std::max(0, std::min(16, atoi(getenv("MSM_HORNER_THREADS")))) : 2;
+  return v;
+}
+
 void pt_to_be_affine(const Pt& p, uint32_t out[16]) {
   uint64_t x[4], y[4];
   pt_to_affine_std(p, x, y);
@@ -1094,7 +1183,7 @@ Segment* get_segment(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const
   Segment* hit = nullptr;
   for (Segment& sg : sl.seg)
     if (sg.exec && sg.parts == parts && sg.pts_buf == pts && sg.acc_events == acc_events && sg.gen == gen &&
-        plan_eq(sg.pl, pl))
+        sg.fork == slot_forks(sl) && plan_eq(sg.pl, pl))
       hit = &sg;
   if (!hit) {
     Segment* victim = &sl.seg[0];
@@ -1110,6 +1199,7 @@ Segment* get_segment(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const
     victim->parts = parts;
     victim->pts_buf = pts;
     victim->acc_events = acc_events;
+    victim->fork = slot_forks(sl);
     victim->gen = gen;
     int rc = capture(c, pl, d_points, d_scalars, si, sl.stream, parts, pts, acc_events, &victim->graph,
                      &victim->exec);
@@ -1142,17 +1232,14 @@ Segment* get_segment(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const
 // runtime cannot capture event records, the accumulation is launched eagerly between a graph of
 // the parts before it and one of the parts after it.  Profiling mode 1 launches everything
 // eagerly with an event between every phase.
-int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
-                 int parts, uint32_t* pts) {
-  Slot& sl = c->slot[si];
-  hipStream_t s = sl.stream;
+int launch_on(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, int parts,
+              uint32_t* pts, hipStream_t s) {
   // k_accumulate's bracketing events only when profiling mode 2 reads them: each event-record
   // node adds ~6 us to the launch sequence's critical path (profiles/r3/latency_timeline.txt)
   const bool acc = (parts & PART_ACC) != 0 && c->profiling == 2;
-  sl.acc_timed = acc;
-  if (c->profiling && (parts & (PART_PREP | PART_SORT))) HIPCHECK(hipEventRecord(sl.ev_start, s));
+  if (parts & PART_ACC) c->slot[si].acc_timed = acc;
   if (c->profiling == 1) {
-    sl.acc_timed = false;
+    c->slot[si].acc_timed = false;
     if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts)) return rc;
   } else if (c->graphs_ok && graphs_enabled()) {
     Segment* sg = (!acc || c->graph_events_ok) ? get_segment(c, pl, d_points, d_scalars, si, parts, pts, acc) : nullptr;
@@ -1171,11 +1258,20 @@ int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Bat
       if (int rc = run(parts & (PART_PREP | PART_SORT))) return rc;
       if (parts & PART_ACC)
         if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, PART_ACC, pts, acc)) return rc;
-      if (int rc = run(parts & PART_POST)) return rc;
+      if (int rc = run(parts & (PART_POST | PART_JOIN))) return rc;
     }
   } else if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts, acc)) {
     return rc;
   }
+  return MSM_OK;
+}
+
+int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
+                 int parts, uint32_t* pts) {
+  Slot& sl = c->slot[si];
+  hipStream_t s = sl.stream;
+  if (c->profiling && (parts & (PART_PREP | PART_SORT))) HIPCHECK(hipEventRecord(sl.ev_start, s));
+  if (int rc = launch_on(c, pl, d_points, d_scalars, si, parts, pts, s)) return rc;
   if (parts & PART_POST) {
     if (c->profiling) HIPCHECK(hipEventRecord(sl.ev_end, s));
     HIPCHECK(hipEventRecord(sl.ev_done, s));
@@ -1344,6 +1440,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   int rc = make_plan(n, o, c->shape, &pl);
   if (rc != MSM_OK) return rc;
   const int si = 0;  // a lone MSM always uses slot 0 (the other workspaces only for pipelining)
+  c->slot[si].pipelined = false;
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = order_after_user(c, user_stream, 1)) != MSM_OK) return rc;
   c->slot[si].pl = pl;
@@ -1409,6 +1506,7 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   if (rc != MSM_OK) return rc;
   const int si = 0;
   Slot& sl = c->slot[si];
+  sl.pipelined = false;
   Workspace& w = sl.ws;
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = w.wire_pts.ensure(n * 128)) != MSM_OK || (rc = w.wire_sc.ensure(n * 32)) != MSM_OK) return rc;
@@ -1483,6 +1581,9 @@ struct ManyInputs {
   uint32_t batch = 0;                        // MSMs per launch (0: pipeline_batch's choice)
   const size_t* lens = nullptr;  // host inputs: real points per MSM (<= n; the rest is padded on
                                  // the device with identity points and zero scalars); null: all n
+  const uint32_t* const* dev_points = nullptr;  // host inputs: per MSM, the device buffer (n points,
+                                                // its own, never reused in the call) their points are
+                                                // uploaded into instead of the slot's wire buffer
   const uint32_t* const* dev_scalars = nullptr;  // host inputs whose scalars are already on the
                                                  // device (n + padding words per MSM): no scalar upload
 };
@@ -1526,6 +1627,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   const int want = pipeline_slots(n, o) + (host && !(o && (o->flags & MSM_FLAG_SERIAL)) && !getenv("MSM_SLOTS") ? 1 : 0);
   const int nslot = nbatch > 1 ? (int)std::min<size_t>(nbatch, (size_t)std::min(want, NSLOT)) : 1;
   for (int si = 0; si < nslot; si++) {
+    c->slot[si].pipelined = nslot > 1;
     if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
     if (host) {
       Workspace& w = c->slot[si].ws;
@@ -1573,19 +1675,19 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       if (host) {  // padding MSMs of a short last launch read the last real MSM's wire buffers
         const uint32_t mr = std::min<uint32_t>(m, nreal - 1);
         bs->p[m] = in.dev_scalars ? in.dev_scalars[j * nm + mr] : sl.ws.wire_sc.as<uint32_t>() + (size_t)mr * n * 8;
-        if (!shared) bp->p[m] = sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
+        if (!shared)
+          bp->p[m] = in.dev_points ? in.dev_points[j * nm + mr] : sl.ws.wire_pts.as<uint32_t>() + (size_t)mr * n * 32;
       }
     }
     return nreal;
   };
   // Host inputs of launch j into its slot's wire buffers, on the copy stream: the scalars, the
-  // device padding of short MSMs, an event on the scalars (ev_sc), the points, an event on all of
-  // them (ev_in).  MSMs whose host arrays are adjacent (the slices of run_host_split) go up in one
+  // device padding of short MSMs, an event on the scalars (up_ev[2 j]), the points, an event on all
+  // of them (up_ev[2 j + 1]).  MSMs whose host arrays are adjacent (the slices of run_host_split) go up in one
   // copy per array: each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between
   // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
   // up alone and its tail is padded on the device.
   auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
-    Slot& sl = c->slot[j % nslot];
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
     auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
@@ -1614,10 +1716,10 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         if (hipGetLastError() != hipSuccess) return MSM_ERR_HIP;
       }
     }
-    HIPCHECK(hipEventRecord(sl.ev_sc, c->copy_stream));
+    HIPCHECK(hipEventRecord(c->up_ev[2 * j], c->copy_stream));
     scalars_done();
     if (!shared && !up(in.points, bp, 32)) return MSM_ERR_HIP;
-    HIPCHECK(hipEventRecord(sl.ev_in, c->copy_stream));
+    HIPCHECK(hipEventRecord(c->up_ev[2 * j + 1], c->copy_stream));
     return MSM_OK;
   };
   // With host inputs and more than one launch, a helper thread (the uploader) issues every
@@ -1628,6 +1730,16 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // only after its previous launch is done with them: the copy stream waits for that launch's
   // ev_done, recorded once this thread has enqueued it (`enqueued`).
   const bool uploader = host && nbatch > 1;
+  // Inputs uploaded into buffers of their own (dev_points / dev_scalars, never reused within the
+  // call) need no wait for a slot's previous launch: the copies then run back to back.
+  const bool own_buffers = (shared || in.dev_points) && in.dev_scalars;
+  if (host) {
+    while (c->up_ev.size() < 2 * nbatch) {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MSM_ERR_HIP;
+      c->up_ev.push_back(e);
+    }
+  }
   std::atomic<size_t> sc_ready{0}, up_ready{0}, enqueued{0};
   std::atomic<int> up_rc{MSM_OK};
   std::atomic<bool> up_stop{false};
@@ -1648,9 +1760,14 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   if (tail_helpers() > 0 && !c->crew) c->crew = new TailCrew(tail_helpers());
   TailCrew* crew = tail_helpers() > 0 ? c->crew : nullptr;
   bool crew_armed = false;
+  // and the pool the earlier launches' tails (their terms copied out per launch)
+  if (horner_threads() > 0 && !c->pool) c->pool = new HornerPool(horner_threads());
+  HornerPool* pool = horner_threads() > 0 ? c->pool : nullptr;
+  std::vector<std::vector<uint32_t>> launch_terms(pool ? nbatch : 0);
   auto fail = [&](int code) {
     if (crew_armed) crew->disarm();  // no terms will come
     crew_armed = false;
+    if (pool) pool->wait_all();  // its jobs read launch_terms
     stop_uploader();
     hipStreamSynchronize(c->copy_stream);
     for (int k = 0; k < nslot; k++) hipStreamSynchronize(c->slot[k].stream);
@@ -1661,7 +1778,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       hipSetDevice(c->device);
       for (size_t j = 0; j < nbatch && !up_stop.load(); j++) {
         int urc = MSM_OK;
-        if (j >= (size_t)nslot) {
+        if (j >= (size_t)nslot && !own_buffers) {
           // launch j - nslot (the slot's previous one) must have been enqueued before its
           // ev_done can be waited for
           while (enqueued.load(std::memory_order_acquire) < j - nslot + 1 && !up_stop.load()) std::this_thread::yield();
@@ -1685,7 +1802,10 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   for (size_t j = 0; j < nbatch + nslot; j++) {
     const bool have = j >= (size_t)nslot;
     const size_t f = have ? j - nslot : 0;
-    if (have && (rc = finish_msm(c, (int)(f % nslot), nullptr, &terms)) != MSM_OK) return fail(rc);
+    // the last launch's terms stay in `terms` (its tails run here, over the crew); the pool's jobs
+    // read their launch's own copy
+    std::vector<uint32_t>* tdst = pool && have && f + 1 < nbatch ? &launch_terms[f] : &terms;
+    if (have && (rc = finish_msm(c, (int)(f % nslot), nullptr, tdst)) != MSM_OK) return fail(rc);
     if (j < nbatch) {
       const int si = (int)(j % nslot);
       Slot& sl = c->slot[si];
@@ -1700,12 +1820,12 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         if (!uploader && (rc = upload_launch(j, [] {})) != MSM_OK) return fail(rc);
         if (sort_early) {
           if (uploader && !wait_for(sc_ready, j + 1)) return fail(up_rc.load());
-          if (hipStreamWaitEvent(sl.stream, sl.ev_sc, 0) != hipSuccess) return fail(MSM_ERR_HIP);
+          if (hipStreamWaitEvent(sl.stream, c->up_ev[2 * j], 0) != hipSuccess) return fail(MSM_ERR_HIP);
           sl.pl = pl;
           if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
         }
         if (uploader && !wait_for(up_ready, j + 1)) return fail(up_rc.load());
-        if (hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess) return fail(MSM_ERR_HIP);
+        if (hipStreamWaitEvent(sl.stream, c->up_ev[2 * j + 1], 0) != hipSuccess) return fail(MSM_ERR_HIP);
       }
       sl.pl = pl;
       if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
@@ -1719,6 +1839,13 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     if (have) {
       const uint32_t k = (uint32_t)std::min<size_t>(nm, count - f * nm);
       Pt res[MSM_MAX_BATCH];
+      if (pool && f + 1 < nbatch) {
+        // off this thread: the next launch's enqueue must not wait for these tails
+        const uint32_t* tp = launch_terms[f].data();
+        for (uint32_t m = 0; m < k; m++)
+          pool->push([&, tp, f, m] { emit(horner_tail(pl, tp, m), f * nm + m); });
+        continue;
+      }
       if (crew_armed && f + 1 == nbatch) {
         // the last launch's tails are the pipeline's drain, on the critical path of the call: their
         // window sums over the device context's helpers, the k outer Horners side by side
@@ -1734,6 +1861,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       for (uint32_t m = 0; m < k; m++) emit(res[m], f * nm + m);
     }
   }
+  if (pool) pool->wait_all();
   stop_uploader();  // its last copies were waited for by the last launch
   return MSM_OK;
 }
@@ -1796,6 +1924,20 @@ bool host_scalars_first() {
   return on;
 }
 
+// Points per slice of the split's last launch (MSM_HOST_TAIL_LOG; 0 = none): round 4 measured
+// such tails slower (one more launch, and the copies waited for slots); re-measured with the
+// call's own upload buffers.
+size_t host_tail() {
+  static const size_t v = getenv("MSM_HOST_TAIL_LOG") && atoi(getenv("MSM_HOST_TAIL_LOG")) > 0
+                              ? (size_t)1 << atoi(getenv("MSM_HOST_TAIL_LOG")) : 0;
+  return v;
+}
+
+bool host_own_points() {
+  static const bool on = !(getenv("MSM_HOST_OWN_PTS") && atoi(getenv("MSM_HOST_OWN_PTS")) == 0);
+  return on;
+}
+
 int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* o,
                    Pt* result) {
   // G <= 16 balanced slices of s points, a whole number of launches of nmb slices (every slice
@@ -1803,14 +1945,23 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   // with identity points and zero scalars, which add no bucket entries).  (Short tail slices for
   // the last launch -- its compute is what is left after the last upload -- measured slower: one
   // more launch costs more than the shorter tail saves)
+  // With MSM_HOST_TAIL_LOG = k the last launch instead holds nmb short slices of 2^k points (the
+  // body then n - nmb 2^k points in Gb balanced slices): its compute after the last upload shrinks.
   const uint32_t nmb = host_batch();
-  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, n / host_piece()));
+  size_t t = host_tail();
+  if (t * nmb * 8 > n) t = 0;  // small MSMs: no tail launch
+  const size_t body = n - t * nmb;
+  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, body / host_piece()));
   Gb = (Gb + nmb - 1) / nmb * nmb;
-  const size_t s = (n + Gb - 1) / Gb;
+  const size_t s = (body + Gb - 1) / Gb;
   std::vector<size_t> offs, lens;
   for (size_t g = 0; g < Gb; g++) {
-    offs.push_back(std::min(g * s, n));
-    lens.push_back(g * s < n ? std::min(s, n - g * s) : 0);  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
+    offs.push_back(std::min(g * s, body));
+    lens.push_back(g * s < body ? std::min(s, body - g * s) : 0);  // 0 only for tiny MSM_HOST_PIECE_LOG overrides
+  }
+  for (size_t g = 0; t && g < nmb; g++) {
+    offs.push_back(body + g * t);
+    lens.push_back(t);
   }
   const size_t G = offs.size();
   std::vector<const uint32_t*> pp(G), ss(G);
@@ -1845,6 +1996,18 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
     }
     for (size_t g = 0; g < G; g++) dsc[g] = base + g * s * 8;
     in.dev_scalars = dsc.data();
+  }
+  // the points into a buffer of the call's own as well (slice g at g s, with room for its device
+  // padding): the uploader then never waits for a slot's previous launch before a copy, so the
+  // copy engine runs the whole upload back to back (MSM_HOST_OWN_PTS=0: the slots' wire buffers)
+  std::vector<const uint32_t*> dpt(G);
+  if (host_scalars_first() && host_own_points()) {
+    if (int rc = c->host_pts.ensure(G * s * 128)) {
+      hipStreamSynchronize(c->copy_stream);  // the scalar copy reads the caller's array
+      return rc;
+    }
+    for (size_t g = 0; g < G; g++) dpt[g] = c->host_pts.as<uint32_t>() + g * s * 32;
+    in.dev_points = dpt.data();
   }
   // The slices' window: that of a 2^17 slice (c = 15) whatever their length.  n not a multiple of
   // 2^18 makes slices a little short of 2^17 (2^20 - 524 points: 131,007), where pipelined_window
@@ -2139,6 +2302,7 @@ void msm_shutdown(void) {
     for (Slot& sl : c->slot) hipStreamSynchronize(sl.stream);
     c->shared_pts.release();
     c->host_sc.release();
+    c->host_pts.release();
     for (Slot& sl : c->slot) {
       sl.ws.release();
       for (Segment& sg : sl.seg) sg.drop();
@@ -2160,6 +2324,10 @@ void msm_shutdown(void) {
     hipStreamDestroy(c->copy_stream);
     delete c->crew;
     c->crew = nullptr;
+    delete c->pool;
+    c->pool = nullptr;
+    for (hipEvent_t e : c->up_ev) hipEventDestroy(e);
+    c->up_ev.clear();
     hipSetDevice(prev);
   }
   for (DevCtx*& c : g_ctx) {
