@@ -1565,6 +1565,19 @@ uint32_t pipeline_batch(size_t n, size_t count) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
+// Pipelined launches: whether launch j's accumulation waits for launch j - 1's reduction
+// (MSM_ACC_AFTER_PREV, default on).  k_accumulate fills every CU's LDS and VGPRs for its whole
+// length, so a kernel queued behind one of its waves gets CUs only in its tail: a kernel trace of
+// the 2^20 bench showed the previous launch's k_bucket_reduce_1 stretched from 161 to ~1,500 us
+// beside the next accumulation, its slot finishing late and the slot's next sort then running
+// alone between two accumulations (profiles/r5/pipeline_gap.txt).  Ordered this way the reduction
+// runs in the gap right after its own accumulation, and the next launch's sort -- HBM and LDS
+// work, which the accumulation leaves idle -- has a whole accumulation to finish beside it.
+bool acc_after_prev() {
+  static const bool on = !(getenv("MSM_ACC_AFTER_PREV") && atoi(getenv("MSM_ACC_AFTER_PREV")) == 0);
+  return on;
+}
+
 // Whether a host-input pipelined run starts its last launch's sort before that launch's points
 // upload (MSM_HOST_SORT_EARLY=0 disables, for A/B runs).
 bool host_sort_early() {
@@ -1828,8 +1841,18 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         if (hipStreamWaitEvent(sl.stream, c->up_ev[2 * j + 1], 0) != hipSuccess) return fail(MSM_ERR_HIP);
       }
       sl.pl = pl;
-      if ((rc = launch_parts(c, pl, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
+      const int lp = sort_early ? parts & ~PART_SORT : parts;
+      if (j >= 1 && nslot > 1 && acc_after_prev() && (lp & PART_ACC)) {
+        // the accumulation waits for the previous launch's reduction (its ev_done), the sort does
+        // not: the reduction never starves behind this accumulation (acc_after_prev)
+        const int pre = lp & (PART_PREP | PART_SORT);
+        if (pre && (rc = launch_parts(c, pl, bp, bs, si, pre, pts)) != MSM_OK) return fail(rc);
+        if (hipStreamWaitEvent(sl.stream, c->slot[(j - 1) % nslot].ev_done, 0) != hipSuccess)
+          return fail(MSM_ERR_HIP);
+        if ((rc = launch_parts(c, pl, bp, bs, si, lp & ~pre, pts)) != MSM_OK) return fail(rc);
+      } else if ((rc = launch_parts(c, pl, bp, bs, si, lp, pts)) != MSM_OK) {
         return fail(rc);
+      }
       enqueued.store(j + 1, std::memory_order_release);
       if (crew && j + 1 == nbatch) {
         crew->arm();  // spins while the device runs the last launch

@@ -223,7 +223,10 @@ __device__ __forceinline__ pre load_pre_signed(const uint32_t* __restrict__ pts,
 template <typename F>
 __device__ __forceinline__ void recode(uint32_t s[8], const MsmDims& d, F&& f) {
   uint32_t carry = 0;
-  for (uint32_t w = 0; w < d.Wm; w++) {
+  // carries only climb: a window range's digits need the windows below it, never those above
+  // (a lower share of a windows split stops at its top window)
+  const uint32_t wend = d.w0 + d.Wr;
+  for (uint32_t w = 0; w < wend; w++) {
     const uint32_t b = win_bits(d, w);
     const uint32_t half = 1u << (b - 1);
     const uint32_t v = (s[0] & ((1u << b) - 1u)) + carry;
