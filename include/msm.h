@@ -9,7 +9,10 @@
  *
  * Wire formats (identical to the reference's, src/submission/consts.ts:1-4, bytes.rs:11-71):
  *   field element : 8 x uint32, BIG-endian word order (index 0 = most significant), standard form
- *   point         : x | y | t | z  = 32 x uint32 = 128 B   (t = x*y/z, z usually 1)
+ *   point         : x | y | t | z  = 32 x uint32 = 128 B   (t = x*y/z, z usually 1); every
+ *                   coordinate must be < p (MSM_ERR_COORD_RANGE otherwise), but the MSM itself
+ *                   uses only x, y and z -- d t is recomputed from the affine x y, as the oracle
+ *                   (Aleo's msm over affine points) does, so an inconsistent t does not change it
  *   scalar        : 8 x uint32 big-endian = full 256-bit integer (not reduced mod r)
  *   result        : x | y affine = 16 x uint32; identity = (0, 1)
  */
@@ -131,7 +134,9 @@ uint32_t msm_best_window(size_t n);
  * like the oracle's empty `Address.msm`.  Uploads overlap compute (generalises the reference's
  * staging ring, gpu.ts:146-155 / 244-271): from n = 3 * 2^17 the MSM runs as point slices of ~2^17
  * through the pipelined launches, slice g+1 uploading on a copy stream while slice g computes,
- * and the slices' partials are joined (the shard/join identity of submission.ts:116-154);
+ * and the slices' partials are joined (the shard/join identity of submission.ts:116-154); there
+ * the library's threads pack x|y of every point (x|y|z for a launch with some z != 1) into pinned
+ * staging -- half the PCIe bytes -- and check every t < p on the host;
  * smaller MSMs upload the scalars first (the bucket sort starts on them) and the points in 8 MiB
  * pieces, each prepared as it lands.  The caller keeps ownership of the arrays; they are not read
  * after the call returns. */

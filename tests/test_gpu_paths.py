@@ -73,6 +73,29 @@ def test_host_split_projective_points():
     assert M.compute_msm_wire(M.gen_points(n, k0=9, step=7), sc) == exp
 
 
+@pytest.mark.parametrize("n", [1000, (1 << 19) + 5])
+def test_t_is_checked_but_not_used(n):
+    """Every entry derives d t from the affine x and y (the oracle reads only (x, y)): a record with
+    an inconsistent t < p gives the same result, and t >= p is still MSM_ERR_COORD_RANGE -- on
+    the device-resident entry and from host arrays, where the split path (n >= 3 x 2^17) uploads
+    only x|y (packed by the library's threads) and checks t on the host."""
+    pts = M.gen_points(n, k0=4, step=9)
+    sc = M.gen_scalars(n, seed=5 + n % 3)
+    exp = closed_form(4, 9, sc)
+    bad_t = pts.copy()
+    for i in (0, n // 2, n - 1):
+        bad_t[i, 16:24] = np.uint32(0x01234567) ^ np.arange(8, dtype=np.uint32)  # t < p, not x y
+    assert M.compute_msm_wire(bad_t, sc) == exp
+    assert M.compute_msm_device(_dev(bad_t), _dev(sc), n) == exp
+    over = pts.copy()
+    over[n - 2, 16:24] = 0xFFFFFFFF  # t >= p
+    for fn in (lambda: M.compute_msm_wire(over, sc), lambda: M.compute_msm_device(_dev(over), _dev(sc), n)):
+        with pytest.raises(M.MsmError) as e:
+            fn()
+        assert e.value.code == -3
+    assert M.compute_msm_wire(pts, sc) == exp  # recovers
+
+
 def test_host_many_distinct():
     cases = []
     for j, n in enumerate((3000, 3000, 3000, 3000, 3000)):

@@ -156,6 +156,31 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamDestroy(s2));
   }
+  // strided: only part of every 128-B point record (x|y = 64 B and z = 32 B of x|y|t|z: t
+  // derived on the device) by 2D copies from the pageable array -- payload GB/s against the whole
+  // 128-B records' contiguous copy
+  for (int variant = 0; variant < 3; variant++) {
+    const size_t pts = total / 128;
+    double best = 1e9;
+    for (int r = 0; r < 3; r++) {
+      auto t0 = clk::now();
+      if (variant == 0) {  // x|y only
+        CK(hipMemcpy2DAsync(dev, 64, host, 128, 64, pts, hipMemcpyHostToDevice, s));
+      } else if (variant == 1) {  // x|y and z: two 2D copies into two device arrays
+        CK(hipMemcpy2DAsync(dev, 64, host, 128, 64, pts, hipMemcpyHostToDevice, s));
+        CK(hipMemcpy2DAsync((char*)dev + pts * 64, 32, host + 96, 128, 32, pts, hipMemcpyHostToDevice, s));
+      } else {  // x|y|t (96 B) in one 2D copy
+        CK(hipMemcpy2DAsync(dev, 96, host, 128, 96, pts, hipMemcpyHostToDevice, s));
+      }
+      CK(hipStreamSynchronize(s));
+      best = std::min(best, ms_since(t0));
+    }
+    static const char* names[3] = {"strided_xy", "strided_xy_and_z", "strided_xyt"};
+    const size_t payload = variant == 0 ? pts * 64 : pts * 96;
+    char ex[128];
+    snprintf(ex, sizeof ex, ", \"payload_GBps\": %.1f, \"payload_MiB\": %zu", payload / best / 1e6, payload / MB);
+    rep(names[variant], best, ex);
+  }
   // pinned source
   char* pin;
   auto tp = clk::now();
@@ -241,6 +266,56 @@ int main(int argc, char** argv) {
       snprintf(ex, sizeof ex, ", \"threads\": %d, \"chunk_MiB\": %zu", th, chunk / MB);
       rep("staged_ring", best, ex);
       for (int k = 0; k < NST; k++) hipEventDestroy(ev[k]);
+    }
+  }
+  // packed ring: pool threads copy only x|y (64 of every 128 B) -- or x|y|z (96) -- of the
+  // pageable records into pinned chunks, each chunk DMAed while the next is packed: the compact
+  // host upload (t is derived on the device; z only when some point has z != 1)
+  for (int keep : {64, 96}) {
+    for (int th : {4, 8, 16}) {
+      Pool pool(th);
+      const size_t pts = total / 128;
+      for (size_t chunk_pts : {size_t(1) << 17, size_t(1) << 18}) {
+        const int NST = 3;
+        hipEvent_t ev[NST];
+        for (int k = 0; k < NST; k++) CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+        double best = 1e9;
+        for (int r = 0; r < 3; r++) {
+          auto t0 = clk::now();
+          bool used[NST] = {};
+          int k = 0;
+          for (size_t p0 = 0; p0 < pts; p0 += chunk_pts, k = (k + 1) % NST) {
+            const size_t np = std::min(chunk_pts, pts - p0);
+            if (used[k]) CK(hipEventSynchronize(ev[k]));
+            char* dst = pin + k * chunk_pts * keep;
+            const char* srcp = host + p0 * 128;
+            // strided pack across the pool's threads
+            std::atomic<int> done{0};
+            auto work = [&](size_t lo, size_t hi) {
+              for (size_t i = lo; i < hi; i++) {
+                memcpy(dst + i * keep, srcp + i * 128, 64);
+                if (keep == 96) memcpy(dst + i * keep + 64, srcp + i * 128 + 96, 32);
+              }
+            };
+            std::vector<std::thread> ts;
+            const size_t per = (np + th - 1) / th;
+            for (int t = 1; t < th; t++) ts.emplace_back(work, std::min(np, t * per), std::min(np, (t + 1) * per));
+            work(0, std::min(np, per));
+            for (auto& t : ts) t.join();
+            (void)done;
+            CK(hipMemcpyAsync((char*)dev + p0 * keep, dst, np * keep, hipMemcpyHostToDevice, s));
+            CK(hipEventRecord(ev[k], s));
+            used[k] = true;
+          }
+          CK(hipStreamSynchronize(s));
+          best = std::min(best, ms_since(t0));
+        }
+        char ex[160];
+        snprintf(ex, sizeof ex, ", \"keep_B\": %d, \"threads\": %d, \"chunk_points\": %zu, \"records_per_ms\": %.0f",
+                 keep, th, chunk_pts, pts / best);
+        rep("packed_ring", best, ex);
+        for (int q = 0; q < NST; q++) hipEventDestroy(ev[q]);
+      }
     }
   }
   // pinned source, chunked DMA (the pinned-input fast path)

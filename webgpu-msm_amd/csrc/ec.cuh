@@ -7,7 +7,7 @@
 // (curve.wgsl:36-63) computes the same group law with 9 multiplies; here:
 //   * madd (mixed, Q in halved precomputed affine form ((y-x)/2, (y+x)/2, d*t), z = 1): 7M — the
 //     bucket hot loop;
-//   * padd (projective + projective): 9M, signed differences like madd;
+//   * padd (projective + projective): 9M;
 //   * pdbl (dbl-2008-hwcd): 4M + 4S.
 #pragma once
 #include "fp29.cuh"
@@ -53,24 +53,21 @@ __device__ __forceinline__ xyzt pt_madd(const xyzt& p, const pre& q) {
 }
 
 // p + q, both extended projective.  add-2008-hwcd-3, k = 2d: 9M (the k multiply is fe_mul_2d).
-// Round 5: the differences are signed (fe_sub_s, as in pt_madd) and meet fe_mul_sd, with
-// D = 2 Z1 Z2 normalised so that F = D - C has limbs in (-2^29, 2^29) and G = D + C is an S-form
-// sum: every multiply keeps all eight 32-bit reduction digits (tests/test_limb_bounds.py
-// test_padd_bounds), and the three 5p offsets and F's renormalisation are gone.
 __device__ __forceinline__ xyzt pt_add(const xyzt& p, const xyzt& q) {
-  fe A = fe_mul_sd<WIDE_ALL, true>(fe_sub_s(p.Y, p.X), fe_sub_s(q.Y, q.X));  // signed x signed
+  fe A = fe_mul_w<WIDE_EF>(fe_sub_v(p.Y, p.X), fe_sub_v(q.Y, q.X));  // V*V
   fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));  // S*S
   fe C = fe_mul_2d(fe_mul(p.T, q.T));  // k = 2d = 6042: scaled, not multiplied (value < 3p)
-  fe D = fe_dbl_n(fe_mul(p.Z, q.Z));   // 2 Z1 Z2, normalised (value < 4p)
-  fe E = fe_sub_s(B, A);  // signed
-  fe F = fe_sub_s(D, C);  // signed
-  fe G = fe_add(D, C);    // S
+  fe D = fe_mul(p.Z, q.Z);
+  D = fe_add(D, D);  // 2N, unnormalised
+  fe E = fe_sub_v(B, A);  // V
+  fe F = fe_sub(D, C);    // N
+  fe G = fe_add(D, C);    // 2N + N: limbs < 1.5 * 2^30 (meets H: S and F: N only)
   fe H = fe_add(B, A);    // S
   xyzt r;
-  r.X = fe_mul_sd<WIDE_ALL, true>(E, F);   // signed x signed
-  r.Y = fe_mul(G, H);                      // S x S
-  r.T = fe_mul_sd<WIDE_ALL, false>(E, H);  // signed x S
-  r.Z = fe_mul_sd<WIDE_ALL, false>(F, G);  // signed x S
+  r.X = fe_mul(E, F);             // V x N
+  r.Y = fe_mul_w<WIDE_GH>(G, H);  // 1.5-form x S: fewer 32-bit reduction digits (fp29.cuh)
+  r.T = fe_mul(E, H);             // V x S
+  r.Z = fe_mul(F, G);
   return r;
 }
 

@@ -27,6 +27,8 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "../../include/msm.h"
 #include "hostfield.h"
 #include "msm_cpu.h"
@@ -129,6 +131,7 @@ struct Plan {
   uint32_t nterms;  // nv + bits of the largest chunk index
   size_t Mmax;      // W * n upper bound on sorted entries
   size_t runs_max;
+  uint32_t pfmt;    // input point format of k_prepare_points (PT_FMT_*: wire records or a compact upload)
 };
 
 // Every field that shapes a launch (grids, buffer offsets, the h_out layout): a captured graph is
@@ -141,7 +144,7 @@ bool plan_eq(const Plan& a, const Plan& b) {
          x.nhi == y.nhi && x.fb == y.fb && x.nbc == y.nbc && x.nbins == y.nbins && x.ch == y.ch && x.nch == y.nch &&
          x.packed == y.packed && x.shared == y.shared && a.K == b.K && a.L == b.L &&
          a.nchunks == b.nchunks && a.nv == b.nv && a.nterms == b.nterms && a.Mmax == b.Mmax &&
-         a.runs_max == b.runs_max;
+         a.runs_max == b.runs_max && a.pfmt == b.pfmt;
 }
 
 // Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
@@ -220,6 +223,18 @@ constexpr int NCHUNK_EV = 8;  // events marking uploaded point chunks
 
 class TailCrew;
 class HornerPool;
+class PackPool;
+
+// Pinned staging buffers of the packed host upload (run_host_split with host_pack()): the
+// library's own threads write compacted points (and the scalars) into them, the copy engine
+// reads them (a DMA from pinned memory needs no staging by the runtime), each buffer reused once
+// the copy out of it has completed (ev).
+constexpr int NPIN = 3;
+struct PinRing {
+  HostBuf buf[NPIN];
+  hipEvent_t ev[NPIN] = {};
+  bool used[NPIN] = {};
+};
 
 // What the launch plans take from the device: compute units, and k_accumulate's waves per SIMD
 // (the occupancy query at context creation; run_length_for fills whole rounds of them).  The test
@@ -241,6 +256,8 @@ struct DevCtx {
   Buf shared_pts;  // point records of a shared base vector (msm_compute_shared*)
   Buf host_sc;     // all the scalars of a split host-input MSM (run_host_split), uploaded first
   Buf host_pts;    // and all its points, slice by slice (no slot buffer reused within the call)
+  PinRing pin;     // pinned staging of the packed host upload
+  PackPool* packer = nullptr;  // its packing threads (persistent, created on first use)
   hipEvent_t ev[PH_COUNT] = {};  // per-phase events (profiling mode 1)
   int profiling = 0;  // 0 off, 1 every phase (eager launches), 2 k_accumulate + device total per launch
   // The launch sequence of each slot is captured into HIP graphs and replayed: one
@@ -586,9 +603,13 @@ bool fork_prepare() {
   static const bool on = !(getenv("MSM_FORK_PREP") && atoi(getenv("MSM_FORK_PREP")) == 0);
   return on;
 }
-// The same for the launches of a pipelined run (MSM_FORK_PREP_PIPE, default on).
+// The same for the launches of a pipelined run (MSM_FORK_PREP_PIPE=1; default off).  There the fork
+// measured slower: 2^20 at 20 steps 1.010 against 1.044 ms per MSM, three interleaved rounds each
+// (and 1.022 against 1.035 in another session, profiles/r5/pipeline_ab.jsonl) -- a captured graph's
+// forked branch runs on a hardware queue of the runtime's choosing, which the other slot's launch
+// may be using (kernel traces show both slots' kernels on the same queues).
 bool fork_prepare_pipelined() {
-  static const bool on = !(getenv("MSM_FORK_PREP_PIPE") && atoi(getenv("MSM_FORK_PREP_PIPE")) == 0);
+  static const bool on = getenv("MSM_FORK_PREP_PIPE") && atoi(getenv("MSM_FORK_PREP_PIPE")) != 0;
   return on;
 }
 bool slot_forks(const Slot& sl) { return sl.pipelined ? fork_prepare() && fork_prepare_pipelined() : fork_prepare(); }
@@ -608,7 +629,7 @@ void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint3
   BatchPtrs bp{};
   bp.p[0] = wire;
   hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(cnt, PP_THREADS), 1), dim3(PP_THREADS), 0, s, bp, pts_out, cnt,
-                     err, nt);
+                     err, nt, PT_FMT_WIRE);
 }
 
 // Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
@@ -640,7 +661,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
       ps = sl.aux;
     }
     hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, ps,
-                       d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n));
+                       d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n), pl.pfmt);
     if (fork) HIPCHECK(hipEventRecord(sl.ev_join, sl.aux));
     mark(PH_PREPARE);
   }
@@ -1008,6 +1029,144 @@ class HornerPool {
   bool quit_ = false;
 };
 
+// The packed host upload's threads: run(fn) calls fn(k, K) on K threads (the caller is k = 0) and
+// returns when all are done.  Workers spin briefly between jobs, then sleep.
+class PackPool {
+ public:
+  explicit PackPool(int threads) : k_(std::max(1, threads)) {
+    for (int i = 1; i < k_; i++) th_.emplace_back([this, i] { work(i); });
+  }
+  ~PackPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  int size() const { return k_; }
+  void run(const std::function<void(int, int)>& fn) {
+    fn_ = &fn;
+    done_.store(0);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      gen_++;
+    }
+    cv_.notify_all();
+    fn(0, k_);
+    while (done_.load(std::memory_order_acquire) < k_ - 1) _mm_pause();
+  }
+
+ private:
+  void work(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (quit_) return;
+      }
+      (*fn_)(i, k_);
+      done_.fetch_add(1, std::memory_order_release);
+    }
+  }
+  int k_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint64_t gen_ = 0;
+  bool quit_ = false;
+  const std::function<void(int, int)>* fn_ = nullptr;
+  std::atomic<int> done_{0};
+};
+
+// Whether run_host_split packs its points (MSM_HOST_PACK, default on): the library's threads copy
+// only x|y of every 128-B record (or x|y|z when some point of a launch has z != 1) into pinned
+// staging, and t is derived from x and y on the device -- half the PCIe bytes of the points.
+bool host_pack() {
+  static const bool on = !(getenv("MSM_HOST_PACK") && atoi(getenv("MSM_HOST_PACK")) == 0);
+  return on;
+}
+int pack_threads() {
+  static const int v = getenv("MSM_HOST_PACK_THREADS") ? std::max(1, std::min(32, atoi(getenv("MSM_HOST_PACK_THREADS")))) : 8;
+  return v;
+}
+
+// t < p for a coordinate in BE words (t is not uploaded by the packed path, so its range is
+// checked here: the reference panics on any coordinate >= p, bytes.rs:19).
+inline bool be_lt_p(const uint32_t* w) {
+  static const uint32_t PBE[8] = {0x12ab655eu, 0x9a2ca556u, 0x60b44d1eu, 0x5c37b001u,
+                                  0x59aa76feu, 0xd0000001u, 0x0a118000u, 0x00000001u};
+  for (int k = 0; k < 8; k++)
+    if (w[k] != PBE[k]) return w[k] < PBE[k];
+  return false;
+}
+
+// One thread's share of pack_records: records [lo, hi).  32-B loads from the caller's array and
+// nontemporal 32-B stores into the pinned staging (no read-for-ownership of the lines written;
+// the staging is only read again by the copy engine).  dst is 32-B aligned (a pinned buffer at a
+// multiple of 64 B).
+__attribute__((target("avx2"))) void pack_range(uint32_t* dst, const uint32_t* src, size_t lo, size_t hi, uint32_t fmt,
+                                                bool* z_other, bool* t_bad) {
+  const size_t pw = pt_fmt_slots(fmt) * 4;
+  bool zo = false, bad = false;
+  for (size_t i = lo; i < hi; i++) {
+    const uint32_t* r = src + i * 32;
+    __m256i* d = reinterpret_cast<__m256i*>(dst + i * pw);
+    _mm256_stream_si256(d, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(r)));
+    _mm256_stream_si256(d + 1, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(r + 8)));
+    if (fmt == PT_FMT_XYZ) _mm256_stream_si256(d + 2, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(r + 24)));
+    zo = zo || r[31] != 1u || (r[24] | r[25] | r[26] | r[27] | r[28] | r[29] | r[30]) != 0u;
+    bad = bad || (r[16] >= 0x12ab655eu && !be_lt_p(r + 16));
+  }
+  _mm_sfence();
+  *z_other = zo;
+  *t_bad = bad;
+}
+
+// Pack cnt wire records (x|y|t|z, 32 BE words) into dst in format fmt (PT_FMT_XY: x|y, 16 words;
+// PT_FMT_XYZ: x|y|z, 24 words) over the pool; returns whether every z is 1 (XY is then exact)
+// and sets *t_bad when some t >= p.
+bool pack_records(PackPool& pool, uint32_t* dst, const uint32_t* src, size_t cnt, uint32_t fmt, bool* t_bad) {
+  std::atomic<bool> z_other{false}, tb{false};
+  pool.run([&](int k, int K) {
+    const size_t lo = cnt * k / K, hi = cnt * (k + 1) / K;
+    bool zo = false, bad = false;
+    pack_range(dst, src, lo, hi, fmt, &zo, &bad);
+    if (zo) z_other.store(true, std::memory_order_relaxed);
+    if (bad) tb.store(true, std::memory_order_relaxed);
+  });
+  if (tb.load()) *t_bad = true;
+  return !z_other.load();
+}
+
+// Plain parallel copy into pinned staging (the packed path's scalars).
+void pack_copy(PackPool& pool, void* dst, const void* src, size_t bytes) {
+  pool.run([&](int k, int K) {
+    const size_t lo = (bytes * k / K) & ~size_t(63), hi = k + 1 == K ? bytes : (bytes * (k + 1) / K) & ~size_t(63);
+    if (hi > lo) memcpy(static_cast<char*>(dst) + lo, static_cast<const char*>(src) + lo, hi - lo);
+  });
+}
+
+// The next staging buffer of the ring, at least `bytes` long, once the copy out of it is done.
+int pin_take(DevCtx* c, int k, size_t bytes, void** out) {
+  PinRing& r = c->pin;
+  if (!r.ev[k] && hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming) != hipSuccess) return MSM_ERR_HIP;
+  if (r.used[k] && hipEventSynchronize(r.ev[k]) != hipSuccess) return MSM_ERR_HIP;
+  r.used[k] = false;
+  if (int rc = r.buf[k].ensure(bytes)) return rc;
+  *out = r.buf[k].p;
+  return MSM_OK;
+}
+// The copy out of buffer k is enqueued on `s`: it is reusable once that completes.
+int pin_give(DevCtx* c, int k, hipStream_t s) {
+  if (hipEventRecord(c->pin.ev[k], s) != hipSuccess) return MSM_ERR_HIP;
+  c->pin.used[k] = true;
+  return MSM_OK;
+}
+
 // Worker threads of the pool (MSM_HORNER_THREADS; 0 = the launching thread runs the tails itself).
 int horner_threads() {
   static const int v =
@@ -1152,7 +1311,8 @@ int repoint_inputs(const Plan& pl, Slot& sl, Segment& sg, const BatchPtrs& d_poi
     uint32_t n = d.n;
     uint32_t* err = w.err.as<uint32_t>();
     uint32_t nt = prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n);
-    void* a_prep[] = {&wire, &ptsb, &n, &err, &nt};
+    uint32_t fmt = pl.pfmt;
+    void* a_prep[] = {&wire, &ptsb, &n, &err, &nt, &fmt};
     hipKernelNodeParams kp = sg.p_prep;
     kp.kernelParams = a_prep;
     kp.extra = nullptr;
@@ -1565,19 +1725,6 @@ uint32_t pipeline_batch(size_t n, size_t count) {
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(nm, count));
 }
 
-// Pipelined launches: whether launch j's accumulation waits for launch j - 1's reduction
-// (MSM_ACC_AFTER_PREV, default on).  k_accumulate fills every CU's LDS and VGPRs for its whole
-// length, so a kernel queued behind one of its waves gets CUs only in its tail: a kernel trace of
-// the 2^20 bench showed the previous launch's k_bucket_reduce_1 stretched from 161 to ~1,500 us
-// beside the next accumulation, its slot finishing late and the slot's next sort then running
-// alone between two accumulations (profiles/r5/pipeline_gap.txt).  Ordered this way the reduction
-// runs in the gap right after its own accumulation, and the next launch's sort -- HBM and LDS
-// work, which the accumulation leaves idle -- has a whole accumulation to finish beside it.
-bool acc_after_prev() {
-  static const bool on = !(getenv("MSM_ACC_AFTER_PREV") && atoi(getenv("MSM_ACC_AFTER_PREV")) == 0);
-  return on;
-}
-
 // Whether a host-input pipelined run starts its last launch's sort before that launch's points
 // upload (MSM_HOST_SORT_EARLY=0 disables, for A/B runs).
 bool host_sort_early() {
@@ -1597,6 +1744,9 @@ struct ManyInputs {
   const uint32_t* const* dev_points = nullptr;  // host inputs: per MSM, the device buffer (n points,
                                                 // its own, never reused in the call) their points are
                                                 // uploaded into instead of the slot's wire buffer
+  bool packed = false;  // host points packed by the library's threads into pinned staging (x|y, or
+                        // x|y|z for a launch with some z != 1) and copied into dev_points (24 words
+                        // of room per point); the launch's k_prepare_points reads that format
   const uint32_t* const* dev_scalars = nullptr;  // host inputs whose scalars are already on the
                                                  // device (n + padding words per MSM): no scalar upload
 };
@@ -1700,10 +1850,53 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // copy per array: each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between
   // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
   // up alone and its tail is padded on the device.
+  const bool packed = host && in.packed && in.dev_points && !shared;
+  std::vector<uint32_t> launch_fmt(nbatch, PT_FMT_WIRE);  // the packed launches' point formats
+  std::atomic<bool> t_bad{false};                         // a packed t >= p (MSM_ERR_COORD_RANGE)
+  if (packed && !c->packer) c->packer = new PackPool(pack_threads());
   auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
     auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
+    if (packed) {
+      // the launch's points into pinned staging buffer j % NPIN: x|y if every z is 1, else x|y|z;
+      // one copy per slice into its dev_points region; padding of a short slice in that format
+      HIPCHECK(hipEventRecord(c->up_ev[2 * j], c->copy_stream));  // its scalars went up before the call
+      scalars_done();
+      const int k = (int)(j % NPIN);
+      void* buf;
+      if (int rc = pin_take(c, k, (size_t)nm * n * 96, &buf)) return rc;
+      uint32_t* pb = static_cast<uint32_t*>(buf);
+      uint32_t fmt = PT_FMT_XY;
+      bool tb = false;
+      for (uint32_t m = 0; m < nreal && fmt == PT_FMT_XY; m++) {
+        const size_t b = j * nm + m;
+        if (!pack_records(*c->packer, pb + (size_t)m * n * 16, in.points[b], len_of(b), PT_FMT_XY, &tb)) fmt = PT_FMT_XYZ;
+      }
+      if (fmt == PT_FMT_XYZ)
+        for (uint32_t m = 0; m < nreal; m++) {
+          const size_t b = j * nm + m;
+          pack_records(*c->packer, pb + (size_t)m * n * 24, in.points[b], len_of(b), PT_FMT_XYZ, &tb);
+        }
+      if (tb) t_bad.store(true);
+      const size_t pw = pt_fmt_slots(fmt) * 4;
+      for (uint32_t m = 0; m < nreal; m++) {
+        const size_t b = j * nm + m, len = len_of(b);
+        if (len && hipMemcpyAsync(const_cast<uint32_t*>(bp.p[m]), pb + (size_t)m * n * pw, len * pw * 4,
+                                  hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+          return MSM_ERR_HIP;
+        if (len < n) {
+          hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * (pt_fmt_slots(fmt) + 2), 256)), dim3(256), 0,
+                             c->copy_stream, const_cast<uint32_t*>(bp.p[m]) + len * pw,
+                             const_cast<uint32_t*>(bs.p[m]) + len * 8, (uint32_t)(n - len), fmt);
+          if (hipGetLastError() != hipSuccess) return MSM_ERR_HIP;
+        }
+      }
+      if (int rc = pin_give(c, k, c->copy_stream)) return rc;
+      launch_fmt[j] = fmt;
+      HIPCHECK(hipEventRecord(c->up_ev[2 * j + 1], c->copy_stream));
+      return MSM_OK;
+    }
     auto up = [&](const uint32_t* const* src, const BatchPtrs& dst, size_t per) -> bool {
       for (uint32_t m0 = 0; m0 < nreal;) {
         const size_t b0 = std::min(j * nm + m0, count - 1);
@@ -1725,7 +1918,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       if (len < n) {
         hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * 10, 256)), dim3(256), 0, c->copy_stream,
                            const_cast<uint32_t*>(bp.p[m]) + len * 32, const_cast<uint32_t*>(bs.p[m]) + len * 8,
-                           (uint32_t)(n - len));
+                           (uint32_t)(n - len), PT_FMT_WIRE);
         if (hipGetLastError() != hipSuccess) return MSM_ERR_HIP;
       }
     }
@@ -1840,19 +2033,11 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
         if (uploader && !wait_for(up_ready, j + 1)) return fail(up_rc.load());
         if (hipStreamWaitEvent(sl.stream, c->up_ev[2 * j + 1], 0) != hipSuccess) return fail(MSM_ERR_HIP);
       }
-      sl.pl = pl;
-      const int lp = sort_early ? parts & ~PART_SORT : parts;
-      if (j >= 1 && nslot > 1 && acc_after_prev() && (lp & PART_ACC)) {
-        // the accumulation waits for the previous launch's reduction (its ev_done), the sort does
-        // not: the reduction never starves behind this accumulation (acc_after_prev)
-        const int pre = lp & (PART_PREP | PART_SORT);
-        if (pre && (rc = launch_parts(c, pl, bp, bs, si, pre, pts)) != MSM_OK) return fail(rc);
-        if (hipStreamWaitEvent(sl.stream, c->slot[(j - 1) % nslot].ev_done, 0) != hipSuccess)
-          return fail(MSM_ERR_HIP);
-        if ((rc = launch_parts(c, pl, bp, bs, si, lp & ~pre, pts)) != MSM_OK) return fail(rc);
-      } else if ((rc = launch_parts(c, pl, bp, bs, si, lp, pts)) != MSM_OK) {
+      Plan plj = pl;
+      plj.pfmt = packed ? launch_fmt[j] : PT_FMT_WIRE;  // set by the uploader before up_ready
+      sl.pl = plj;
+      if ((rc = launch_parts(c, plj, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
         return fail(rc);
-      }
       enqueued.store(j + 1, std::memory_order_release);
       if (crew && j + 1 == nbatch) {
         crew->arm();  // spins while the device runs the last launch
@@ -1886,7 +2071,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   }
   if (pool) pool->wait_all();
   stop_uploader();  // its last copies were waited for by the last launch
-  return MSM_OK;
+  return t_bad.load() ? MSM_ERR_COORD_RANGE : MSM_OK;
 }
 
 int with_device(const msm_opts* o, DevCtx** c) {
@@ -2005,15 +2190,45 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
     // slice in its own
     if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
     uint32_t* base = c->host_sc.as<uint32_t>();
+    const bool pack = host_pack() && host_own_points();
+    if (pack && !c->packer) c->packer = new PackPool(pack_threads());
+    if (pack) {
+      // every staging buffer at its largest use (a launch's packed points, the scalar pieces) before
+      // anything is enqueued: a later growth would bump the allocation generation mid-call
+      const size_t need = std::max<size_t>((size_t)8 << 20, (size_t)nmb * s * 96);
+      for (int k = 0; k < NPIN; k++) {
+        void* b;
+        if (int rc = pin_take(c, k, need, &b)) return rc;
+      }
+    }
+    int kpin = 0;
     for (size_t g = 0; g < G;) {
       size_t h = g + 1;
       if (lens[g] == s)
         while (h < G && lens[h] == s && offs[h] == offs[g] + (h - g) * s) h++;
       const size_t words = (h - g == 1 ? lens[g] : (h - g) * s) * 8;
-      if (words && hipMemcpyAsync(base + g * s * 8, scalars_be + offs[g] * 8, words * 4, hipMemcpyHostToDevice,
-                                  c->copy_stream) != hipSuccess) {
-        hipStreamSynchronize(c->copy_stream);
-        return MSM_ERR_HIP;
+      // packed: through the pinned ring in 8 MiB pieces (the library's threads copy, the copy
+      // engine reads pinned memory); otherwise one pageable copy per run of slices
+      const size_t piece = pack ? (size_t)2 << 20 : words;
+      for (size_t w0 = 0; w0 < words; w0 += piece) {
+        const size_t wn = std::min(piece, words - w0);
+        const uint32_t* hsrc = scalars_be + offs[g] * 8 + w0;
+        const void* from = hsrc;
+        if (pack) {
+          void* buf;
+          if (int rc = pin_take(c, kpin, wn * 4, &buf)) {
+            hipStreamSynchronize(c->copy_stream);
+            return rc;
+          }
+          pack_copy(*c->packer, buf, hsrc, wn * 4);
+          from = buf;
+        }
+        if (hipMemcpyAsync(base + g * s * 8 + w0, from, wn * 4, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+            (pack && pin_give(c, kpin, c->copy_stream) != MSM_OK)) {
+          hipStreamSynchronize(c->copy_stream);
+          return MSM_ERR_HIP;
+        }
+        kpin = (kpin + 1) % NPIN;
       }
       g = h;
     }
@@ -2025,12 +2240,15 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   // copy engine runs the whole upload back to back (MSM_HOST_OWN_PTS=0: the slots' wire buffers)
   std::vector<const uint32_t*> dpt(G);
   if (host_scalars_first() && host_own_points()) {
-    if (int rc = c->host_pts.ensure(G * s * 128)) {
+    // packed (host_pack): room for the widest packed form, x|y|z (24 words per point)
+    const size_t pw = host_pack() ? 24 : 32;
+    if (int rc = c->host_pts.ensure(G * s * pw * 4)) {
       hipStreamSynchronize(c->copy_stream);  // the scalar copy reads the caller's array
       return rc;
     }
-    for (size_t g = 0; g < G; g++) dpt[g] = c->host_pts.as<uint32_t>() + g * s * 32;
+    for (size_t g = 0; g < G; g++) dpt[g] = c->host_pts.as<uint32_t>() + g * s * pw;
     in.dev_points = dpt.data();
+    in.packed = host_pack();
   }
   // The slices' window: that of a 2^17 slice (c = 15) whatever their length.  n not a multiple of
   // 2^18 makes slices a little short of 2^17 (2^20 - 524 points: 131,007), where pipelined_window
@@ -2349,6 +2567,14 @@ void msm_shutdown(void) {
     c->crew = nullptr;
     delete c->pool;
     c->pool = nullptr;
+    delete c->packer;
+    c->packer = nullptr;
+    for (int k = 0; k < NPIN; k++) {
+      c->pin.buf[k].release();
+      if (c->pin.ev[k]) hipEventDestroy(c->pin.ev[k]);
+      c->pin.ev[k] = nullptr;
+      c->pin.used[k] = false;
+    }
     for (hipEvent_t e : c->up_ev) hipEventDestroy(e);
     c->up_ev.clear();
     hipSetDevice(prev);

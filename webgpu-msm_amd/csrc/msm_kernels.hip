@@ -67,42 +67,59 @@ constexpr uint32_t PP_THREADS = MSM_PP_THREADS;
 typedef uint32_t pp_v4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t pp_slot(uint32_t rec, uint32_t q) { return rec * 8 + (q ^ (rec & 7)); }
 
+// Input point formats (`fmt`): PT_FMT_WIRE the reference's 128-B x|y|t|z records; the compact
+// forms of host uploads (run_host_split) leave t out -- PT_FMT_XYZ 96 B x|y|z, PT_FMT_XY 64 B x|y
+// with z = 1 -- and the record's d t is derived from x and y (the oracle's own semantics: Aleo's
+// msm reads affine (x, y)).
+constexpr uint32_t PT_FMT_WIRE = 0, PT_FMT_XY = 1, PT_FMT_XYZ = 2;
+__host__ __device__ constexpr uint32_t pt_fmt_slots(uint32_t fmt) {  // 16-B slots per input point
+  return fmt == PT_FMT_XY ? 4u : fmt == PT_FMT_XYZ ? 6u : 8u;
+}
+// Montgomery form of 4d: d t = 4d (x/2)(y/2) from the halved coordinates.
+__device__ constexpr uint32_t K4D29[NL] = {531568572u, 449839103u, 184174685u, 15704447u, 1165364u,
+                                           393938084u, 340476652u, 106785266u, 592681u};
+
 // blockIdx.y = MSM of the batch: its wire points come from wires.p[y], its records go to
 // pts[y n ..).
 extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchPtrs wires,
                                                                           uint32_t* __restrict__ pts, uint32_t n,
-                                                                          uint32_t* __restrict__ err, uint32_t nt) {
+                                                                          uint32_t* __restrict__ err, uint32_t nt,
+                                                                          uint32_t fmt) {
   __shared__ uint4 st[PP_THREADS * 8];
+  const uint32_t S = pt_fmt_slots(fmt);
   const uint32_t p0 = blockIdx.x * PP_THREADS;
   const uint32_t np = min(PP_THREADS, n - p0);
-  const uint4* src = reinterpret_cast<const uint4*>(wires.p[blockIdx.y]) + (size_t)p0 * 8;
+  const uint4* src = reinterpret_cast<const uint4*>(wires.p[blockIdx.y]) + (size_t)p0 * S;
   pts += (size_t)blockIdx.y * n * PRE_WORDS;
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
     const uint32_t g = j * PP_THREADS + threadIdx.x;  // 16-B slot within the block's records
-    if (g < np * 8) st[pp_slot(g >> 3, g & 7)] = src[g];
+    if (g < np * S) st[pp_slot(g / S, g % S)] = src[g];
   }
   __syncthreads();
   const uint32_t i = threadIdx.x;
   const bool live = i < np;
+  const bool has_t = fmt == PT_FMT_WIRE, has_z = fmt != PT_FMT_XY;  // t: range check only
   uint32_t xw[8], yw[8], tw[8], zw[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) xw[k] = yw[k] = tw[k] = zw[k] = 0;
+  zw[0] = 1;
   if (live) {
     uint4 v[8];
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) v[q] = st[pp_slot(i, q)];
-    // big-endian word order: word 0 is the most significant 32 bits (bytes.rs:11-20)
-    uint32_t* dsts[4] = {xw, yw, tw, zw};
+    for (uint32_t q = 0; q < 8; q++) v[q] = q < S ? st[pp_slot(i, q)] : make_uint4(0u, 0u, 0u, 0u);
+    // big-endian word order: word 0 is the most significant 32 bits (bytes.rs:11-20); the
+    // compact forms hold x, y (and z) in that order
+    uint32_t* dsts[4] = {xw, yw, has_t ? tw : zw, zw};
 #pragma unroll
     for (int f = 0; f < 4; f++) {
+      if (f == 3 && !has_t) break;   // x|y|z: z was the third field
+      if (f == 2 && !has_z) break;   // x|y
       const uint4 a = v[2 * f], b = v[2 * f + 1];
       uint32_t* le = dsts[f];
       le[7] = a.x; le[6] = a.y; le[5] = a.z; le[4] = a.w;
       le[3] = b.x; le[2] = b.y; le[1] = b.z; le[0] = b.w;
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; k++) xw[k] = yw[k] = tw[k] = zw[k] = 0;
-    zw[0] = 1;
   }
   __syncthreads();
   bool ok = words_lt_p(xw) && words_lt_p(yw) && words_lt_p(tw) && words_lt_p(zw);
@@ -116,20 +133,21 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
   }
   if (live && z_zero) atomicOr(err, MSM_DEV_ERR_BAD_POINT);
   // the halved record (ec.cuh pt_madd): x/2, y/2 and d*t in Montgomery form
-  fe x, y, kt;
+  // d t is derived from the affine x and y in every format: the input t is range-checked above
+  // but not used, so a record's result depends on (x, y, z) alone, as the oracle's does (Aleo's
+  // msm reads affine points), whichever entry and upload form carried it
+  fe x, y;
   if (z_one) {
     x = fe_mul(fe_from_words_le(xw), fe_const(R2H_29));
     y = fe_mul(fe_from_words_le(yw), fe_const(R2H_29));
-    kt = fe_mul(fe_from_words_le(tw), fe_const(KD_R2_29));
   } else {
     // Projective input (z != 1, README.md:92 allows it): normalise to affine with one inversion.
     fe zi = fe_inv(fe_to_mont(fe_from_words_le(zw)));
     fe zh = fe_mul(zi, fe_const(HALF29));
-    fe t = fe_mul(fe_to_mont(fe_from_words_le(tw)), zi);
     x = fe_mul(fe_to_mont(fe_from_words_le(xw)), zh);
     y = fe_mul(fe_to_mont(fe_from_words_le(yw)), zh);
-    kt = fe_mul(t, fe_const(KD29));
   }
+  const fe kt = fe_mul(fe_mul(x, y), fe_const(K4D29));  // d x y = 4d (x/2)(y/2)
   fe ymx = fe_sub(y, x);
   fe ypx = fe_add_n(y, x);
   uint32_t rec[32];  // layout: msm_dev.h PRE_WORDS
@@ -168,16 +186,23 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
 }
 
 // Pads a short host-input slice on the device (run_host_split with n not a multiple of its slice
-// count): `count` wire points set to the identity (x, y, t, z) = (0, 1, 0, 1) and `count` scalars
-// set to 0, so the padding contributes no bucket entry.  16-B stores, one per thread.
+// count): `count` points set to the identity (x, y, t, z) = (0, 1, 0, 1) -- in the input format
+// `fmt` of the slice's point buffer (wire records, or the compact x|y|z of a compact upload) --
+// and `count` scalars set to 0, so the padding contributes no bucket entry.  16-B stores, one
+// per thread.
 extern "C" __global__ void __launch_bounds__(256) k_pad_identity(uint32_t* __restrict__ wire_pts,
-                                                                   uint32_t* __restrict__ wire_sc, uint32_t count) {
-  const uint32_t g = blockIdx.x * 256 + threadIdx.x;  // 16-B slot: 8 per point, then 2 per scalar
-  if (g < count * 8) {
-    const uint32_t q = g & 7;  // BE words: the least significant word of y (slot 3) and z (slot 7)
-    reinterpret_cast<uint4*>(wire_pts)[g] = make_uint4(0u, 0u, 0u, (q == 3 || q == 7) ? 1u : 0u);
-  } else if (g < count * 10) {
-    reinterpret_cast<uint4*>(wire_sc)[g - count * 8] = make_uint4(0u, 0u, 0u, 0u);
+                                                                   uint32_t* __restrict__ wire_sc, uint32_t count,
+                                                                   uint32_t fmt) {
+  const uint32_t S = pt_fmt_slots(fmt);
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;  // 16-B slot: S per point, then 2 per scalar
+  if (g < count * S) {
+    // BE words: the least significant word of y (slot 3), and of z (the point's last slot) unless
+    // the format has no z
+    const uint32_t q = g % S;
+    const bool one = q == 3 || (fmt != PT_FMT_XY && q == S - 1);
+    reinterpret_cast<uint4*>(wire_pts)[g] = make_uint4(0u, 0u, 0u, one ? 1u : 0u);
+  } else if (g < count * (S + 2)) {
+    reinterpret_cast<uint4*>(wire_sc)[g - count * S] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
