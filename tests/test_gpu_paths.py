@@ -49,10 +49,12 @@ def test_host_entry_split_into_slices(n):
     assert M.combine_partials(np.asarray(part, dtype=np.uint32).reshape(1, 32)) == exp
 
 
-def test_host_split_projective_points():
+@pytest.mark.parametrize("first", [3, None])
+def test_host_split_projective_points(first):
     # the split host path with projective points (z != 1, normalised by k_prepare_points) in one
     # launch's slices and in the short, device-padded last slice; z = 0 in another launch is still
-    # rejected
+    # rejected.  first=None: slice 0 of launch 0 is affine, so it goes up packed as x|y before
+    # slice 1's z != 1 makes the launch repack both as x|y|z and send them again
     from oracle import oracle as O
 
     n = (1 << 19) + 5  # four slices in two launches, the last one short
@@ -60,7 +62,8 @@ def test_host_split_projective_points():
     sc = M.gen_scalars(n, seed=77)
     exp = closed_form(9, 7, sc)
     # projective points in launch 0 (slices 0 and 1) and at the end of the short last slice
-    for i, z in ((3, 2), ((1 << 17) + 11, 12345678901), (n - 1, O.P - 2)):
+    zs = [((1 << 17) + 11, 12345678901), (n - 1, O.P - 2)] + ([(first, 2)] if first is not None else [])
+    for i, z in zs:
         x, y, t = (O.be_words_to_int(pts[i, 8 * j: 8 * j + 8]) for j in range(3))
         for j, v in enumerate((x * z % O.P, y * z % O.P, t * z % O.P, z)):
             pts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)

@@ -78,6 +78,8 @@ for step in "$@"; do
     tests_alt)
       MSM_NO_GRAPH=1 run tests_eager 900 "${PYTEST[@]}" -k "not random_sweep"
       MSM_SLOTS=1 MSM_BATCH=1 run tests_1slot 900 "${PYTEST[@]}" -k "not random_sweep" ;;
+    testk:*)  # testk:EXPR -- the GPU tests selected by pytest -k EXPR
+      run testk 900 "${PYTEST[@]}" -k "${step#testk:}" ;;
     testslib:*)
       IFS=: read -r _ libs <<< "$step"
       for lib in ${libs//,/ }; do

@@ -1106,7 +1106,8 @@ inline bool be_lt_p(const uint32_t* w) {
 
 // One thread's share of pack_records: records [lo, hi).  32-B loads from the caller's array and
 // nontemporal 32-B stores into the pinned staging (no read-for-ownership of the lines written;
-// the staging is only read again by the copy engine).  dst is 32-B aligned (a pinned buffer at a
+// the staging is only read again by the copy engine; cached stores measured the same,
+// profiles/r5/e2e_pack.jsonl).  dst is 32-B aligned (a pinned buffer at a
 // multiple of 64 B).
 __attribute__((target("avx2"))) void pack_range(uint32_t* dst, const uint32_t* src, size_t lo, size_t hi, uint32_t fmt,
                                                 bool* z_other, bool* t_bad) {
@@ -1859,35 +1860,58 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
     auto len_of = [&](size_t b) { return in.lens ? std::min(in.lens[b], n) : n; };
     if (packed) {
-      // the launch's points into pinned staging buffer j % NPIN: x|y if every z is 1, else x|y|z;
-      // one copy per slice into its dev_points region; padding of a short slice in that format
-      HIPCHECK(hipEventRecord(c->up_ev[2 * j], c->copy_stream));  // its scalars went up before the call
-      scalars_done();
+      // the launch's scalars, then its points, through pinned staging buffer j % NPIN (points at
+      // [0, 24 nm n) words, scalars after them): the scalars first, each slice's into its
+      // dev_scalars region, so the sort can start; the points as x|y if every z is 1, else x|y|z,
+      // one copy per slice into its dev_points region; a short slice's padding in that format
       const int k = (int)(j % NPIN);
       void* buf;
-      if (int rc = pin_take(c, k, (size_t)nm * n * 96, &buf)) return rc;
+      if (int rc = pin_take(c, k, (size_t)nm * n * 128, &buf)) return rc;
       uint32_t* pb = static_cast<uint32_t*>(buf);
+      uint32_t* psc = pb + (size_t)nm * n * 24;
+      for (uint32_t m = 0; m < nreal; m++) {
+        const size_t b = j * nm + m, len = len_of(b);
+        if (!len) continue;
+        pack_copy(*c->packer, psc + (size_t)m * n * 8, in.scalars[b], len * 32);
+        if (hipMemcpyAsync(const_cast<uint32_t*>(bs.p[m]), psc + (size_t)m * n * 8, len * 32, hipMemcpyHostToDevice,
+                           c->copy_stream) != hipSuccess)
+          return MSM_ERR_HIP;
+        // a short slice's scalar tail is zero before the sort may start (k_pad_identity below
+        // pads its points)
+        if (len < n && hipMemsetAsync(const_cast<uint32_t*>(bs.p[m]) + len * 8, 0, (n - len) * 32, c->copy_stream) !=
+                           hipSuccess)
+          return MSM_ERR_HIP;
+      }
+      HIPCHECK(hipEventRecord(c->up_ev[2 * j], c->copy_stream));
+      scalars_done();
+      // each slice's x|y goes up as soon as it is packed; a z != 1 anywhere in the launch repacks
+      // every slice as x|y|z and sends it again over the same regions (stream order)
       uint32_t fmt = PT_FMT_XY;
       bool tb = false;
+      auto send = [&](uint32_t m) -> bool {
+        const size_t len = len_of(j * nm + m), pw = pt_fmt_slots(fmt) * 4;
+        return !len || hipMemcpyAsync(const_cast<uint32_t*>(bp.p[m]), pb + (size_t)m * n * pw, len * pw * 4,
+                                      hipMemcpyHostToDevice, c->copy_stream) == hipSuccess;
+      };
       for (uint32_t m = 0; m < nreal && fmt == PT_FMT_XY; m++) {
-        const size_t b = j * nm + m;
-        if (!pack_records(*c->packer, pb + (size_t)m * n * 16, in.points[b], len_of(b), PT_FMT_XY, &tb)) fmt = PT_FMT_XYZ;
+        if (!pack_records(*c->packer, pb + (size_t)m * n * 16, in.points[j * nm + m], len_of(j * nm + m), PT_FMT_XY,
+                          &tb))
+          fmt = PT_FMT_XYZ;
+        else if (!send(m))
+          return MSM_ERR_HIP;
       }
       if (fmt == PT_FMT_XYZ)
         for (uint32_t m = 0; m < nreal; m++) {
           const size_t b = j * nm + m;
           pack_records(*c->packer, pb + (size_t)m * n * 24, in.points[b], len_of(b), PT_FMT_XYZ, &tb);
+          if (!send(m)) return MSM_ERR_HIP;
         }
       if (tb) t_bad.store(true);
-      const size_t pw = pt_fmt_slots(fmt) * 4;
       for (uint32_t m = 0; m < nreal; m++) {
-        const size_t b = j * nm + m, len = len_of(b);
-        if (len && hipMemcpyAsync(const_cast<uint32_t*>(bp.p[m]), pb + (size_t)m * n * pw, len * pw * 4,
-                                  hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
-          return MSM_ERR_HIP;
+        const size_t len = len_of(j * nm + m);
         if (len < n) {
           hipLaunchKernelGGL(k_pad_identity, dim3(grid_for((n - len) * (pt_fmt_slots(fmt) + 2), 256)), dim3(256), 0,
-                             c->copy_stream, const_cast<uint32_t*>(bp.p[m]) + len * pw,
+                             c->copy_stream, const_cast<uint32_t*>(bp.p[m]) + len * pt_fmt_slots(fmt) * 4,
                              const_cast<uint32_t*>(bs.p[m]) + len * 8, (uint32_t)(n - len), fmt);
           if (hipGetLastError() != hipSuccess) return MSM_ERR_HIP;
         }
@@ -2184,51 +2208,35 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   in.batch = nmb;
   in.lens = lens.data();
   std::vector<const uint32_t*> dsc(G);
-  if (host_scalars_first()) {
+  const bool pack = host_scalars_first() && host_own_points() && host_pack();
+  if (pack) {
+    // packed: every launch's scalars and points go up through the pinned ring from the uploader,
+    // scalars first (run_many), into these device regions (slice g at g s)
+    if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
+    if (!c->packer) c->packer = new PackPool(pack_threads());
+    // every staging buffer at its size before anything is enqueued: a later growth would bump
+    // the allocation generation mid-call
+    for (int k = 0; k < NPIN; k++) {
+      void* b;
+      if (int rc = pin_take(c, k, (size_t)nmb * s * 128, &b)) return rc;
+    }
+    for (size_t g = 0; g < G; g++) dsc[g] = c->host_sc.as<uint32_t>() + g * s * 8;
+    in.dev_scalars = dsc.data();
+  } else if (host_scalars_first()) {
     // slice g's scalars at g s in one device buffer (s words each, the tail of a short slice is
     // its device padding): the run of full slices at the front goes up in one copy, every other
     // slice in its own
     if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
     uint32_t* base = c->host_sc.as<uint32_t>();
-    const bool pack = host_pack() && host_own_points();
-    if (pack && !c->packer) c->packer = new PackPool(pack_threads());
-    if (pack) {
-      // every staging buffer at its largest use (a launch's packed points, the scalar pieces) before
-      // anything is enqueued: a later growth would bump the allocation generation mid-call
-      const size_t need = std::max<size_t>((size_t)8 << 20, (size_t)nmb * s * 96);
-      for (int k = 0; k < NPIN; k++) {
-        void* b;
-        if (int rc = pin_take(c, k, need, &b)) return rc;
-      }
-    }
-    int kpin = 0;
     for (size_t g = 0; g < G;) {
       size_t h = g + 1;
       if (lens[g] == s)
         while (h < G && lens[h] == s && offs[h] == offs[g] + (h - g) * s) h++;
       const size_t words = (h - g == 1 ? lens[g] : (h - g) * s) * 8;
-      // packed: through the pinned ring in 8 MiB pieces (the library's threads copy, the copy
-      // engine reads pinned memory); otherwise one pageable copy per run of slices
-      const size_t piece = pack ? (size_t)2 << 20 : words;
-      for (size_t w0 = 0; w0 < words; w0 += piece) {
-        const size_t wn = std::min(piece, words - w0);
-        const uint32_t* hsrc = scalars_be + offs[g] * 8 + w0;
-        const void* from = hsrc;
-        if (pack) {
-          void* buf;
-          if (int rc = pin_take(c, kpin, wn * 4, &buf)) {
-            hipStreamSynchronize(c->copy_stream);
-            return rc;
-          }
-          pack_copy(*c->packer, buf, hsrc, wn * 4);
-          from = buf;
-        }
-        if (hipMemcpyAsync(base + g * s * 8 + w0, from, wn * 4, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
-            (pack && pin_give(c, kpin, c->copy_stream) != MSM_OK)) {
-          hipStreamSynchronize(c->copy_stream);
-          return MSM_ERR_HIP;
-        }
-        kpin = (kpin + 1) % NPIN;
+      if (words && hipMemcpyAsync(base + g * s * 8, scalars_be + offs[g] * 8, words * 4, hipMemcpyHostToDevice,
+                                  c->copy_stream) != hipSuccess) {
+        hipStreamSynchronize(c->copy_stream);
+        return MSM_ERR_HIP;
       }
       g = h;
     }
@@ -2240,15 +2248,15 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   // copy engine runs the whole upload back to back (MSM_HOST_OWN_PTS=0: the slots' wire buffers)
   std::vector<const uint32_t*> dpt(G);
   if (host_scalars_first() && host_own_points()) {
-    // packed (host_pack): room for the widest packed form, x|y|z (24 words per point)
-    const size_t pw = host_pack() ? 24 : 32;
+    // packed: room for the widest packed form, x|y|z (24 words per point)
+    const size_t pw = pack ? 24 : 32;
     if (int rc = c->host_pts.ensure(G * s * pw * 4)) {
       hipStreamSynchronize(c->copy_stream);  // the scalar copy reads the caller's array
       return rc;
     }
     for (size_t g = 0; g < G; g++) dpt[g] = c->host_pts.as<uint32_t>() + g * s * pw;
     in.dev_points = dpt.data();
-    in.packed = host_pack();
+    in.packed = pack;
   }
   // The slices' window: that of a 2^17 slice (c = 15) whatever their length.  n not a multiple of
   // 2^18 makes slices a little short of 2^17 (2^20 - 524 points: 131,007), where pipelined_window
