@@ -76,6 +76,29 @@ def test_host_split_projective_points(first):
     assert M.compute_msm_wire(M.gen_points(n, k0=9, step=7), sc) == exp
 
 
+def test_host_lone_pieces_mixed_formats():
+    # the lone host path (n < 3 x 2^17) packs each 2^16-point piece on its own: x|y for the affine
+    # pieces, x|y|z for a piece with some z != 1, each prepared in its format; t >= p anywhere is
+    # still MSM_ERR_COORD_RANGE, and the next call is clean
+    from oracle import oracle as O
+
+    n = (1 << 17) + 777  # pieces 0, 1 full, piece 2 short
+    pts = M.gen_points(n, k0=6, step=11)
+    sc = M.gen_scalars(n, seed=19)
+    exp = closed_form(6, 11, sc)
+    for i, z in (((1 << 16) + 3, 99), (n - 1, O.P - 5)):  # pieces 1 and 2 projective, piece 0 affine
+        x, y, t = (O.be_words_to_int(pts[i, 8 * j: 8 * j + 8]) for j in range(3))
+        for j, v in enumerate((x * z % O.P, y * z % O.P, t * z % O.P, z)):
+            pts[i, 8 * j: 8 * j + 8] = O.int_to_be_words(v)
+    assert M.compute_msm_wire(pts, sc) == exp
+    bad = pts.copy()
+    bad[5, 16:24] = O.int_to_be_words(O.P)  # t = p in the affine piece
+    with pytest.raises(M.MsmError) as e:
+        M.compute_msm_wire(bad, sc)
+    assert e.value.code == -3  # MSM_ERR_COORD_RANGE
+    assert M.compute_msm_wire(pts, sc) == exp
+
+
 @pytest.mark.parametrize("n", [1000, (1 << 19) + 5])
 def test_t_is_checked_but_not_used(n):
     """Every entry derives d t from the affine x and y (the oracle reads only (x, y)): a record with

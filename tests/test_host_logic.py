@@ -331,3 +331,36 @@ def test_run_length_past_a_power_of_two():
     assert M.launch_plan(1 << 17, 4, True)["run_length"] == 36
     # an explicit run length is taken as given
     assert M.launch_plan((1 << 20) + 1, 2, True, run_length=44)["run_length"] == 44
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 4099])
+def test_host_packing_keeps_x_y_and_checks_t(n):
+    """The packed uploads' host pass (pack_records, msm_test_pack; run on the library's own
+    threads): x|y (16 words) or x|y|z (24 words) of every wire record, in order, whatever the
+    share boundaries of the threads; `all z == 1` is exact (z has 8 words), and any t >= p is
+    reported (t is checked on the host because it is not uploaded)."""
+    rng = np.random.default_rng(n + 3)
+    wire = np.zeros((n, 32), np.uint32)
+    for i in range(n):
+        for j in range(3):  # x, y, t < p
+            wire[i, 8 * j: 8 * j + 8] = O.int_to_be_words(int(rng.integers(0, 1 << 62)) * 0x1f3 % O.P + j)
+        wire[i, 24:32] = O.int_to_be_words(1)
+    for xyz in (False, True):
+        out, z1, tb = M.pack_points(wire, xyz=xyz)
+        assert out.shape == (n, 24 if xyz else 16)
+        assert np.array_equal(out[:, :16], wire[:, :16])
+        if xyz:
+            assert np.array_equal(out[:, 16:], wire[:, 24:32])
+        assert z1 and not tb
+    if n == 0:
+        return
+    k = n // 2
+    w2 = wire.copy()
+    w2[k, 24:32] = O.int_to_be_words(1 + (1 << 200))  # z != 1 only in a high word
+    out, z1, tb = M.pack_points(w2, xyz=True)
+    assert not z1 and not tb and np.array_equal(out[:, 16:], w2[:, 24:32])
+    for tv, bad in ((O.P - 1, False), (O.P, True), ((1 << 256) - 1, True)):
+        w3 = wire.copy()
+        w3[n - 1, 16:24] = O.int_to_be_words(tv)
+        _, z1, tb = M.pack_points(w3)
+        assert z1 and tb == bad

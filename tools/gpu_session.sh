@@ -156,6 +156,9 @@ for step in "$@"; do
       run e2etrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
         -d gpurun_out/${TAG}_e2etrace_d -o run -- python3 tools/e2e_probe.py --runs 8 ;;
     e2e) run e2e 120 python tools/e2e_probe.py --runs 12 ;;
+    e2esz:*)  # e2esz:NAME:SIZES -- tools/e2e_size_probe.py over the listed sizes (under the current set: knobs)
+      IFS=: read -r _ nm sz <<< "$step"
+      run "e2esz_$nm" 300 python tools/e2e_size_probe.py --sizes "$sz" --runs 7 --rounds 1 ;;
     e2esrc)  # msm_compute from host arrays in numpy / no-huge-page / MAP_SHARED memory
       for src in numpy nohuge shared; do run "e2e_$src" 120 python tools/e2e_probe.py --runs 10 --src "$src"; done ;;
     h2d) run h2d 120 tools/ubench/h2d_bench ;;

@@ -625,11 +625,11 @@ uint32_t prep_nt(size_t records) {
 // k_prepare_points over `cnt` points of one wire buffer into `pts_out` (one MSM, or one uploaded
 // chunk of it); `nt` from prep_nt of the whole record buffer.
 void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint32_t* err, uint32_t nt,
-                    hipStream_t s) {
+                    hipStream_t s, uint32_t fmt = PT_FMT_WIRE) {
   BatchPtrs bp{};
   bp.p[0] = wire;
   hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(cnt, PP_THREADS), 1), dim3(PP_THREADS), 0, s, bp, pts_out, cnt,
-                     err, nt, PT_FMT_WIRE);
+                     err, nt, fmt);
 }
 
 // Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
@@ -1681,12 +1681,59 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
     hipStreamSynchronize(sl.stream);
     return code;
   };
-  if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK) return fail(rc);
-  if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
-  if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) != MSM_OK)
-    return fail(rc);
+  bool t_bad = false;  // some t >= p, checked on the host (t is not uploaded): reported once the
+                       // MSM has run, so the device's flags end cleared as after any call
+  if (host_pack()) {
+    // packed (as the split, §2.6): the scalars through the pinned ring, then each 8 MiB piece of
+    // points as x|y (x|y|z for a piece with some z != 1), prepared in its own format as it lands
+    if (!c->packer) c->packer = new PackPool(pack_threads());
+    int k = 0;
+    uint32_t* wsc = w.wire_sc.as<uint32_t>();
+    for (size_t off = 0; off < n; off += UPLOAD_PTS_PIECE, k++) {
+      const size_t cnt = std::min(UPLOAD_PTS_PIECE, n - off);
+      void* buf;
+      if ((rc = pin_take(c, k % NPIN, cnt * 32, &buf)) != MSM_OK) return fail(rc);
+      pack_copy(*c->packer, buf, scalars_be + off * 8, cnt * 32);
+      if (hipMemcpyAsync(wsc + off * 8, buf, cnt * 32, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+        return fail(MSM_ERR_HIP);
+      if ((rc = pin_give(c, k % NPIN, c->copy_stream)) != MSM_OK) return fail(rc);
+    }
+    if (hipEventRecord(sl.ev_in, c->copy_stream) != hipSuccess || hipStreamWaitEvent(sl.stream, sl.ev_in, 0) != hipSuccess)
+      return fail(MSM_ERR_HIP);
+    if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
+    bool tb = false;
+    uint32_t* wp = w.wire_pts.as<uint32_t>();
+    for (size_t p0 = 0; p0 < n; p0 += UPLOAD_PTS_PIECE, k++) {
+      const size_t cnt = std::min(UPLOAD_PTS_PIECE, n - p0);
+      void* buf;
+      if ((rc = pin_take(c, k % NPIN, cnt * 96, &buf)) != MSM_OK) return fail(rc);
+      uint32_t fmt = PT_FMT_XY;
+      if (!pack_records(*c->packer, static_cast<uint32_t*>(buf), points_be + p0 * 32, cnt, PT_FMT_XY, &tb)) {
+        fmt = PT_FMT_XYZ;
+        pack_records(*c->packer, static_cast<uint32_t*>(buf), points_be + p0 * 32, cnt, PT_FMT_XYZ, &tb);
+      }
+      const size_t pw = pt_fmt_slots(fmt) * 4;
+      if (hipMemcpyAsync(wp + p0 * 24, buf, cnt * pw * 4, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess)
+        return fail(MSM_ERR_HIP);
+      if ((rc = pin_give(c, k % NPIN, c->copy_stream)) != MSM_OK) return fail(rc);
+      hipEvent_t e = c->ev_chunk[k % NCHUNK_EV];
+      if (hipEventRecord(e, c->copy_stream) != hipSuccess || hipStreamWaitEvent(sl.stream, e, 0) != hipSuccess)
+        return fail(MSM_ERR_HIP);
+      launch_prepare(wp + p0 * 24, pts + p0 * PRE_WORDS, (uint32_t)cnt, w.err.as<uint32_t>(), prep_nt(n), sl.stream, fmt);
+      if (hipGetLastError() != hipSuccess) return fail(MSM_ERR_HIP);
+    }
+    t_bad = tb;
+  } else {
+    if ((rc = upload_scalars(c, scalars_be, n, w.wire_sc.as<uint32_t>(), sl.stream, sl.ev_in)) != MSM_OK)
+      return fail(rc);
+    if ((rc = launch_parts(c, pl, bp, bs, si, PART_SORT, pts)) != MSM_OK) return fail(rc);
+    if ((rc = upload_points(c, points_be, n, w.wire_pts.as<uint32_t>(), pts, w.err.as<uint32_t>(), sl.stream)) !=
+        MSM_OK)
+      return fail(rc);
+  }
   if ((rc = launch_parts(c, pl, bp, bs, si, PART_ACC | PART_POST, pts)) != MSM_OK) return fail(rc);
-  return finish_lone(c, si, result);
+  rc = finish_lone(c, si, result);
+  return rc == MSM_OK && t_bad ? MSM_ERR_COORD_RANGE : rc;
 }
 
 // MSMs kept in flight by the pipelined entries.  Small MSMs are latency-bound (their reduction
@@ -3030,6 +3077,28 @@ int msm_test_plan(size_t n, uint32_t nm, int pipelined, const msm_opts* opts, ui
   if (int rc = make_plan(n, opts, DevShape{}, &pl, pipelined != 0, nm)) return rc;
   const uint32_t v[7] = {pl.d.c, pl.d.Wr, pl.K, pl.L, pl.d.nm, pl.d.nbc, run_length_skew_floor(pl.d)};
   memcpy(out, v, sizeof(v));
+  return MSM_OK;
+}
+
+// The host packing of the packed uploads (pack_records over a pool of MSM_HOST_PACK_THREADS):
+// n wire records -> out (16 words per point for fmt 1 = x|y, 24 for fmt 2 = x|y|z); *all_z_one =
+// whether every z is 1, *t_bad = whether some t >= p.  Host code only (no device needed).
+int msm_test_pack(const uint32_t* wire, size_t n, uint32_t fmt, uint32_t* out, int* all_z_one, int* t_bad) {
+  if ((!wire || !out) && n) return MSM_ERR_INVALID_ARG;
+  if (fmt != PT_FMT_XY && fmt != PT_FMT_XYZ) return MSM_ERR_INVALID_ARG;
+  static std::mutex mu;
+  static PackPool* pool = nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!pool) pool = new PackPool(pack_threads());
+  const size_t bytes = n * pt_fmt_slots(fmt) * 16;
+  void* tmp = aligned_alloc(64, (bytes + 63) / 64 * 64 + 64);  // the nontemporal stores want 32-B alignment
+  if (!tmp) return MSM_ERR_OOM;
+  bool tb = false;
+  const bool z1 = pack_records(*pool, static_cast<uint32_t*>(tmp), wire, n, fmt, &tb);
+  memcpy(out, tmp, bytes);
+  free(tmp);
+  if (all_z_one) *all_z_one = z1 ? 1 : 0;
+  if (t_bad) *t_bad = tb ? 1 : 0;
   return MSM_OK;
 }
 

@@ -135,6 +135,8 @@ def load() -> ctypes.CDLL:
         "msm_test_tail": ([sz, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_tail_words": ([sz], sz),
         "msm_test_plan": ([sz, ctypes.c_uint32, ctypes.c_int, optp, u32p], ctypes.c_int),
+        "msm_test_pack": ([vp, sz, ctypes.c_uint32, vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+                          ctypes.c_int),
         "msm_test_tail_batch": ([sz, ctypes.c_uint32, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_peer_state": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -321,6 +323,19 @@ def launch_plan(n: int, nm: int = 1, pipelined: bool = False, window_size: Optio
                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))), "msm_test_plan")
     return dict(zip(("c", "windows", "run_length", "chunk_len", "msms_per_launch", "coarse_bins", "skew_floor"),
                     (int(v) for v in out)))
+
+
+def pack_points(points_wire, xyz: bool = False) -> Tuple[np.ndarray, bool, bool]:
+    """The packed uploads' host packing (msm_test_pack): wire records -> x|y (or x|y|z) words,
+    whether every z is 1, whether some t >= p.  No GPU needed."""
+    pts = np.ascontiguousarray(_u32(points_wire).reshape(-1, 32))
+    n = pts.shape[0]
+    w = 24 if xyz else 16
+    out = np.zeros((n, w), np.uint32)
+    z1, tb = ctypes.c_int(0), ctypes.c_int(0)
+    _check(load().msm_test_pack(_ptr(pts), n, 2 if xyz else 1, _ptr(out), ctypes.byref(z1), ctypes.byref(tb)),
+           "msm_test_pack")
+    return out, bool(z1.value), bool(tb.value)
 
 
 def window_count(window_size: int) -> int:
