@@ -364,3 +364,70 @@ def test_host_packing_keeps_x_y_and_checks_t(n):
         w3[n - 1, 16:24] = O.int_to_be_words(tv)
         _, z1, tb = M.pack_points(w3)
         assert z1 and tb == bad
+
+
+def _red2_groups_model(T, U, nchunks, g, lg):
+    """k_red2_groups' index algebra (msm_kernels.hip) over integers: the lg steps of in-place
+    adds over the group's 2^lg chunks; returns (V, S, R_0..R_{lg-1})."""
+    ch = 1 << lg
+    A = [T[g * ch + i] if g * ch + i < nchunks else 0 for i in range(ch)]
+    Bv = [U[g * ch + i] if g * ch + i < nchunks else 0 for i in range(ch)]
+    for s in range(lg):
+        lp = lg - 1 - s
+        touched = set()
+        for Q in range((2 + s) << lp):
+            kind, i = Q >> lp, Q & ((1 << lp) - 1)
+            arr = Bv if kind == 1 else A
+            if kind < 2:
+                dst = i << (s + 1)
+                src = dst + (1 << s)
+            else:
+                j = kind - 2
+                l = s - j - 1
+                md = i << (l + 1)
+                ms = md + (1 << l)
+                dst, src = (2 * md + 1) << j, (2 * ms + 1) << j
+            key = (kind == 1, dst), (kind == 1, src)
+            assert not (set(key) & touched), "two tasks of one step share a point"
+            touched |= set(key)
+            arr[dst] += arr[src]
+    return [Bv[0], A[0]] + [A[1 << k] for k in range(lg)]
+
+
+@pytest.mark.parametrize("lg", [6, 7, 8])
+@pytest.mark.parametrize("nchunks", [1, 5, 256, 300, 1821, 2048, 4096])
+def test_red2_group_tree_terms(nchunks, lg):
+    """k_red2_groups + k_red2_terms (the second bucket-reduction stage in two kernels, groups of
+    2^lg chunks, MSM_RG_LOG) give terms with sum_v V_v + sum_k 2^k R_k (times L on the host) =
+    sum_c U_c + sum_c c T_c, modelled over integers with the kernels' own index algebra (group
+    trees in place, the R_k lists at indices whose lowest set bit is 2^k, the terms' group
+    selection)."""
+    rng = np.random.default_rng(nchunks)
+    T = [int(x) for x in rng.integers(0, 1 << 40, nchunks)]
+    U = [int(x) for x in rng.integers(0, 1 << 40, nchunks)]
+    G = (nchunks + (1 << lg) - 1) >> lg
+    grp = [_red2_groups_model(T, U, nchunks, g, lg) for g in range(G)]
+    nv = 2 if nchunks >= 2 else 1
+    cbits = 0
+    while (1 << cbits) < nchunks:
+        cbits += 1
+    total = 0
+    for term in range(nv + cbits):
+        if term < nv:
+            sl = (G + nv - 1) // nv
+            g0 = min(G, term * sl)
+            pts = [grp[g][0] for g in range(g0, min(G, g0 + sl))]
+            total += sum(pts)
+            continue
+        k = term - nv
+        if k < lg:
+            pts = [grp[g][2 + k] for g in range(G)]
+        else:
+            kb = k - lg
+            half = 1
+            while 2 * half < G:
+                half <<= 1
+            gs = [((j >> kb) << (kb + 1)) | (1 << kb) | (j & ((1 << kb) - 1)) for j in range(half)]
+            pts = [grp[g][1] for g in gs if g < G]
+        total += (1 << k) * sum(pts)
+    assert total == sum(U) + sum(c * t for c, t in enumerate(T))

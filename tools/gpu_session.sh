@@ -114,8 +114,8 @@ for step in "$@"; do
         run size$lg 120 python bench.py --steps 50 --warmup 20 --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
         run size${lg}_k20 120 python bench.py --no-extras "${BENCH_Q[@]}" --n $((1 << lg))
       done ;;
-    batch64) run batch64 300 python bench.py --batch 64 --n 262144 ;;
-    batch64d) run batch64d 300 python bench.py --batch 64 --n 262144 --distinct ;;  # distinct base vectors
+    batch64) run "batch64${KS:-}" 300 python bench.py --batch 64 --n 262144 ;;
+    batch64d) run "batch64d${KS:-}" 300 python bench.py --batch 64 --n 262144 --distinct ;;  # distinct base vectors
     gloo8)
       MSM_DIST_BACKEND=gloo OMP_NUM_THREADS=2 run gloo8 400 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 2 \
@@ -124,7 +124,7 @@ for step in "$@"; do
     split) run split 600 python tools/split_probe.py --gpus 8 ;;
     split:*)  # split:D:SPLITS:C -- tools/split_probe.py over D GPUs for the listed PxQ splits at window width C
       IFS=: read -r _ ng sp cw <<< "$step"
-      run "split${ng}_${sp//,/_}_c${cw}" 600 python tools/split_probe.py --gpus "$ng" --splits "$sp" --window "$cw" ;;
+      run "split${ng}_${sp//,/_}_c${cw}${KS:-}" 600 python tools/split_probe.py --gpus "$ng" --splits "$sp" --window "$cw" ;;
     kstats)
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;

@@ -153,10 +153,11 @@ struct Workspace {
   Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets, big_tiles, cursor;
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
   Buf wire_pts, wire_sc;  // device copies of host-resident inputs (msm_compute*, host entries)
+  Buf red_G;               // k_red2_groups' points per (window, group of RG_CH chunks)
   void release() {
     Buf* bufs[] = {&pts, &err, &digits, &colsum, &bin_base, &bin_cur, &part_entry, &part_fine,
                    &sorted_entry, &bucket_start, &run_key, &buckets, &big_tiles, &cursor, &lead_val, &lead_open, &cross_key,
-                   &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T, &wire_pts, &wire_sc};
+                   &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T, &wire_pts, &wire_sc, &red_G};
     for (Buf* b : bufs) b->release();
   }
 };
@@ -541,6 +542,15 @@ int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* p
   return MSM_OK;
 }
 
+// The second bucket-reduction stage as k_red2_groups + k_red2_terms (default; MSM_RED2_TREE=0:
+// k_bucket_reduce_2), for windows of at most RG_MAXG groups of RG_CH chunks (k_bucket_reduce_2
+// past that).  Single stream, 2^20, two MSMs per launch: 50 against 58 us.
+uint32_t red2_groups(const Plan& pl) { return (pl.nchunks + RG_CH - 1) / RG_CH; }
+bool red2_tree(const Plan& pl) {
+  static const bool on = !(getenv("MSM_RED2_TREE") && atoi(getenv("MSM_RED2_TREE")) == 0);
+  return on && red2_groups(pl) <= RG_MAXG;
+}
+
 int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   Slot& sl0 = c->slot[si];
   Workspace& w = sl0.ws;
@@ -575,6 +585,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(g_tkey, pl.runs_max * 4);
   ENS(red_U, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
   ENS(red_T, (size_t)d.W * pl.nchunks * PT_WORDS * 4);
+  if (red2_tree(pl)) ENS(red_G, (size_t)d.W * red2_groups(pl) * RG_OUT * PT_WORDS * 4);
 #undef ENS
   if (g_alloc_gen.load() != gen0) {
     // err, lead_flag and colsum are kept all-zero between MSMs by the kernels themselves
@@ -737,10 +748,21 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                        w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(),
                        w.red_T.as<uint32_t>());
     mark(PH_RED1);
-    hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
-                       w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
-                       w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total, joins ? 1u : 0u,
-                       w.bucket_start.as<uint32_t>(), d.B, reinterpret_cast<uint32_t*>(sl.h_out_dev));
+    if (red2_tree(pl)) {
+      const uint32_t G = red2_groups(pl);
+      hipLaunchKernelGGL(k_red2_groups, dim3(d.W * G), dim3(4 * RG_CH), 0, s, w.red_U.as<uint32_t>(),
+                         w.red_T.as<uint32_t>(), pl.nchunks, G, w.bucket_start.as<uint32_t>(), d.B,
+                         w.red_G.as<uint32_t>());
+      hipLaunchKernelGGL(k_red2_terms, dim3(d.W * pl.nterms), dim3(4 * RG_MAXG), 0, s, w.red_G.as<uint32_t>(), G,
+                         pl.nv, pl.nterms, w.err.as<uint32_t>(), w.lead_flag.as<uint32_t>(),
+                         w.skew_list.as<uint32_t>(), total, joins ? 1u : 0u, w.bucket_start.as<uint32_t>(), d.B,
+                         reinterpret_cast<uint32_t*>(sl.h_out_dev));
+    } else {
+      hipLaunchKernelGGL(k_bucket_reduce_2, dim3(d.W * pl.nterms), dim3(RED2_THREADS), 0, s, w.red_U.as<uint32_t>(),
+                         w.red_T.as<uint32_t>(), pl.nchunks, pl.nv, pl.nterms, w.err.as<uint32_t>(),
+                         w.lead_flag.as<uint32_t>(), w.skew_list.as<uint32_t>(), total, joins ? 1u : 0u,
+                         w.bucket_start.as<uint32_t>(), d.B, reinterpret_cast<uint32_t*>(sl.h_out_dev));
+    }
     mark(PH_RED2);
     mark(PH_READBACK);
   }

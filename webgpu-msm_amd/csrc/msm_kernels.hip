@@ -1356,6 +1356,195 @@ extern "C" __global__ void __launch_bounds__(RED2_THREADS) k_bucket_reduce_2(con
   }
 }
 
+// ---- bucket reduction, second stage in two kernels (k_red2_groups + k_red2_terms) ------------
+// k_bucket_reduce_2 sums, per window, every chunk's U_c once and its T_c once per set bit of c
+// (~6.5 adds per chunk at 2,048 chunks), in trees whose wide levels make it VALU-bound.  Here
+// the chunks of a window go in groups of RG_CH = 2^RG_LOG: k_red2_groups reduces a group in LDS
+// to 2 + RG_LOG points,
+//   V_g = sum U_c,  S_g = sum T_c,  R_{g,k} = sum_{c: bit k of (c - RG_CH g)} T_c  (k < RG_LOG),
+// with ~3 adds per chunk: one tree over U, one over T whose odd operands at level j are exactly
+// R_{g,j}'s points (kept in place, lowest set bit of the index = 2^j), and the R trees run in
+// the same steps as the main trees (RG_LOG steps of <= 2 RG_CH quad-cooperative adds).
+// k_red2_terms then forms the same terms as k_bucket_reduce_2 from <= 64 group points each:
+//   V slices = sum V_g,  R_k = sum_g R_{g,k} (k < RG_LOG),  R_k = sum_{g: bit k-RG_LOG of g} S_g,
+// since sum_c c T_c = sum_g (RG_CH g S_g + sum_k 2^k R_{g,k}).
+#ifndef MSM_RG_LOG
+#define MSM_RG_LOG 7
+#endif
+constexpr uint32_t RG_LOG = MSM_RG_LOG;      // log2 chunks per group
+constexpr uint32_t RG_CH = 1u << RG_LOG;     // chunks per group
+constexpr uint32_t RG_OUT = 2 + RG_LOG;      // points per group: V, S, R_0..R_{RG_LOG-1}
+constexpr uint32_t RG_MAXG = 64;             // groups per window k_red2_terms takes
+
+// Coordinate q (0 X, 1 Y, 2 T, 3 Z) of the identity (0, 1, 0, 1).
+__device__ __forceinline__ fe identity_coord(uint32_t q) { return fe_sel((q & 1u) != 0, fe_zero(), fe_one()); }
+__device__ __forceinline__ fe load_fe_g(const uint32_t* __restrict__ src) {
+  fe a;
+#pragma unroll
+  for (int k = 0; k < NL; k++) a.v[k] = src[k];
+  return a;
+}
+
+// One group's reduction (k_red2_groups): chunks g RG_CH .. of window w from
+// in_U / in_T into shA (T) / shB (U) and the RG_LOG steps; leaves V at shB[0], S at shA[0] and
+// R_k at shA[2^k].  Every thread of the block takes part (4 RG_CH threads, quad Q = chunk).
+__device__ __forceinline__ void red2_group_tree(const uint32_t* __restrict__ in_U, const uint32_t* __restrict__ in_T,
+                                                uint32_t nchunks, uint32_t w, uint32_t g,
+                                                uint32_t (*shA)[PT_WORDS], uint32_t (*shB)[PT_WORDS]) {
+  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const uint32_t c = g * RG_CH + Q;
+  fe u, t;
+  if (c < nchunks) {
+    const size_t off = ((size_t)w * nchunks + c) * PT_WORDS + q * NL;
+    u = load_fe_g(in_U + off);
+    t = load_fe_g(in_T + off);
+  } else {
+    u = t = identity_coord(q);
+  }
+  store_fe_lds(&shB[Q][q * NL], u);
+  store_fe_lds(&shA[Q][q * NL], t);
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t s = 0; s < RG_LOG; s++) {
+    const uint32_t lp = RG_LOG - 1 - s;  // log2 of the pairs per list at this step
+    const uint32_t ntask = (2 + s) << lp;
+    if (Q < ntask) {
+      const uint32_t kind = Q >> lp, i = Q & ((1u << lp) - 1u);
+      uint32_t(*arr)[PT_WORDS] = kind == 1 ? shB : shA;
+      uint32_t dst, srcx;
+      if (kind < 2) {  // the T and U trees: pairs (i 2^(s+1), i 2^(s+1) + 2^s)
+        dst = i << (s + 1);
+        srcx = dst + (1u << s);
+      } else {  // R_j's tree, level s - j - 1, over its list at indices (2 m + 1) 2^j
+        const uint32_t j = kind - 2, l = s - j - 1;
+        const uint32_t md = i << (l + 1), ms = md + (1u << l);
+        dst = (2 * md + 1) << j;
+        srcx = (2 * ms + 1) << j;
+      }
+      const fe r = pt_add_quad(load_fe_lds(&arr[dst][q * NL]), load_fe_lds(&arr[srcx][q * NL]));
+      store_fe_lds(&arr[dst][q * NL], r);  // no other task of this step reads dst or srcx
+    }
+    __syncthreads();
+  }
+}
+
+// Group point idx (0 V, 1 S, 2 + k R_k) of the tree left in shA / shB.
+__device__ __forceinline__ const uint32_t* red2_group_point(uint32_t (*shA)[PT_WORDS], uint32_t (*shB)[PT_WORDS],
+                                                            uint32_t idx) {
+  return idx == 0 ? shB[0] : idx == 1 ? shA[0] : shA[1u << (idx - 2)];
+}
+
+// Which group points make term `term` of a window: point idx of groups g0 + j (or, for the bit
+// terms past RG_LOG, of the j-th group with bit kbit set), j < npts.
+struct Red2Term {
+  uint32_t idx, g0, g1, kbit, npts;
+  bool bitsel;
+};
+__device__ __forceinline__ Red2Term red2_term(uint32_t term, uint32_t nv, uint32_t ngroups) {
+  Red2Term r{0, 0, 0, 0, 0, false};
+  if (term < nv) {
+    const uint32_t sl = (ngroups + nv - 1) / nv;
+    r.g0 = min(ngroups, term * sl);
+    r.g1 = min(ngroups, r.g0 + sl);
+    r.npts = r.g1 - r.g0;
+  } else if (term - nv < RG_LOG) {
+    r.idx = 2 + (term - nv);
+    r.g1 = ngroups;
+    r.npts = ngroups;
+  } else {
+    r.idx = 1;
+    r.kbit = term - nv - RG_LOG;
+    r.bitsel = true;
+    r.npts = 1;  // g = ((j >> kbit) << (kbit + 1)) | (1 << kbit) | (j & (2^kbit - 1)), j < pow2ceil(ngroups) / 2
+    while (2 * r.npts < ngroups) r.npts <<= 1;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t red2_term_group(const Red2Term& t, uint32_t j) {
+  return t.bitsel ? (((j >> t.kbit) << (t.kbit + 1)) | (1u << t.kbit) | (j & ((1u << t.kbit) - 1u))) : t.g0 + j;
+}
+
+// Block 0 of k_red2_terms: the MSM's flags beside the terms (as k_bucket_reduce_2).
+__device__ __forceinline__ void red2_flags(uint32_t nwindows_terms, uint32_t* __restrict__ err,
+                                           uint32_t* __restrict__ lead_flag, uint32_t* __restrict__ skew_list,
+                                           const uint32_t* __restrict__ total, uint32_t final_pass,
+                                           uint32_t* __restrict__ out_host) {
+  const size_t tail = (size_t)nwindows_terms * 32;
+  const bool skew = skew_list[0] != 0 || *lead_flag != 0;
+  out_host[tail] = *err;
+  out_host[tail + 1] = *total;
+  out_host[tail + 2] = (skew && !final_pass) ? 1u : 0u;
+  *err = 0;
+  if (final_pass || !skew) {
+    *lead_flag = 0;
+    skew_list[0] = 0;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(4 * RG_CH) k_red2_groups(const uint32_t* __restrict__ in_U,
+                                                                     const uint32_t* __restrict__ in_T,
+                                                                     uint32_t nchunks, uint32_t ngroups,
+                                                                     const uint32_t* __restrict__ bucket_start,
+                                                                     uint32_t B, uint32_t* __restrict__ out) {
+  __shared__ uint32_t shA[RG_CH][PT_WORDS];  // T, then its partial sums and the R lists in place
+  __shared__ uint32_t shB[RG_CH][PT_WORDS];  // U
+  const uint32_t w = blockIdx.x / ngroups, g = blockIdx.x % ngroups;
+  if (bucket_start[(size_t)w * B] == bucket_start[(size_t)(w + 1) * B]) return;  // empty window: unread
+  red2_group_tree(in_U, in_T, nchunks, w, g, shA, shB);
+  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (Q < RG_OUT) {
+    const fe v = load_fe_lds(red2_group_point(shA, shB, Q) + q * NL);
+    uint32_t* o = out + (((size_t)w * ngroups + g) * RG_OUT + Q) * PT_WORDS + q * NL;
+#pragma unroll
+    for (int k = 0; k < NL; k++) o[k] = v.v[k];
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(4 * RG_MAXG) k_red2_terms(const uint32_t* __restrict__ grp,
+                                                                      uint32_t ngroups, uint32_t nv,
+                                                                      uint32_t nterms, uint32_t* __restrict__ err,
+                                                                      uint32_t* __restrict__ lead_flag,
+                                                                      uint32_t* __restrict__ skew_list,
+                                                                      const uint32_t* __restrict__ total,
+                                                                      uint32_t final_pass,
+                                                                      const uint32_t* __restrict__ bucket_start,
+                                                                      uint32_t B, uint32_t* __restrict__ out_host) {
+  __shared__ uint32_t sh[RG_MAXG][PT_WORDS];
+  const uint32_t w = blockIdx.x / nterms, term = blockIdx.x % nterms;
+  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const bool empty = bucket_start[(size_t)w * B] == bucket_start[(size_t)(w + 1) * B];
+  const Red2Term rt = red2_term(term, nv, ngroups);
+  fe v = identity_coord(q);
+  if (!empty && Q < rt.npts) {
+    const uint32_t g = red2_term_group(rt, Q);
+    if (g < ngroups) v = load_fe_g(grp + (((size_t)w * ngroups + g) * RG_OUT + rt.idx) * PT_WORDS + q * NL);
+  }
+  store_fe_lds(&sh[Q][q * NL], v);
+  __syncthreads();
+  uint32_t half = 1;
+  while (2 * half < rt.npts) half <<= 1;
+  if (empty || rt.npts <= 1) half = 0;
+#pragma unroll 1
+  for (; half >= 1; half >>= 1) {
+    if (Q < half) {
+      const fe r = pt_add_quad(load_fe_lds(&sh[Q][q * NL]), load_fe_lds(&sh[Q + half][q * NL]));
+      store_fe_lds(&sh[Q][q * NL], r);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) {  // as k_bucket_reduce_2: host Montgomery form, straight into pinned memory
+    uint32_t* o = out_host + (size_t)blockIdx.x * 32 + 8 * q;
+    uint32_t wd[8];
+    fe_to_words_le(fe_to_host_mont(load_fe_lds(&sh[0][q * NL])), wd);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = wd[k];
+  }
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) red2_flags(gridDim.x, err, lead_flag, skew_list, total, final_pass, out_host);
+    __threadfence_system();
+  }
+}
+
 // Small utility kernels used by tests: batch field ops / point ops on canonical inputs.
 // op 0: field mul, 1: add, 2: sub, 3: 2d * a (fe_mul_2d); inputs LE standard words [n][8] x2, output [n][8].
 extern "C" __global__ void k_test_field(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
