@@ -1375,6 +1375,9 @@ constexpr uint32_t RG_LOG = MSM_RG_LOG;      // log2 chunks per group
 constexpr uint32_t RG_CH = 1u << RG_LOG;     // chunks per group
 constexpr uint32_t RG_OUT = 2 + RG_LOG;      // points per group: V, S, R_0..R_{RG_LOG-1}
 constexpr uint32_t RG_MAXG = 64;             // groups per window k_red2_terms takes
+#ifndef MSM_RED2_SYSFENCE
+#define MSM_RED2_SYSFENCE 0
+#endif
 
 // Coordinate q (0 X, 1 Y, 2 T, 3 Z) of the identity (0, 1, 0, 1).
 __device__ __forceinline__ fe identity_coord(uint32_t q) { return fe_sel((q & 1u) != 0, fe_zero(), fe_one()); }
@@ -1539,10 +1542,16 @@ extern "C" __global__ void __launch_bounds__(4 * RG_MAXG) k_red2_terms(const uin
 #pragma unroll
     for (int k = 0; k < 8; k++) o[k] = wd[k];
   }
+#if MSM_RED2_SYSFENCE
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) red2_flags(gridDim.x, err, lead_flag, skew_list, total, final_pass, out_host);
     __threadfence_system();
   }
+#else
+  // no system-scope fence per workgroup: the host reads the terms only after the launch's event,
+  // whose completion makes the kernel's writes to pinned memory visible
+  if (threadIdx.x == 0 && blockIdx.x == 0) red2_flags(gridDim.x, err, lead_flag, skew_list, total, final_pass, out_host);
+#endif
 }
 
 // Small utility kernels used by tests: batch field ops / point ops on canonical inputs.
