@@ -105,9 +105,9 @@ struct HostBuf {
     if (p) hipHostFree(p);
     p = nullptr;
     cap = 0;
-    // pinned, host-cacheable memory; k_bucket_reduce_2 writes its results straight into it and
-    // publishes them with __threadfence_system() (a coherent/uncached mapping would make the
-    // host Horner's reads ~4x slower)
+    // pinned, host-cacheable memory; k_red2_terms (or k_bucket_reduce_2) writes its results
+    // straight into it, visible to the host once the launch's event completes (a coherent /
+    // uncached mapping would make the host Horner's reads ~4x slower)
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
       p = nullptr;
       return MSM_ERR_OOM;
