@@ -136,10 +136,12 @@ uint32_t msm_best_window(size_t n);
  * through the pipelined launches, slice g+1 uploading on a copy stream while slice g computes,
  * and the slices' partials are joined (the shard/join identity of submission.ts:116-154); there
  * the library's threads pack x|y of every point (x|y|z for a launch with some z != 1) into pinned
- * staging -- half the PCIe bytes -- and check every t < p on the host;
- * smaller MSMs upload the scalars first (the bucket sort starts on them) and the points in 8 MiB
- * pieces, each prepared as it lands.  The caller keeps ownership of the arrays; they are not read
- * after the call returns. */
+ * staging -- half the PCIe bytes -- and check every t < p on the host; smaller MSMs upload the
+ * scalars first (the bucket sort starts on them) and the points in 2^16-point pieces, packed the
+ * same way per piece, each prepared as it lands.  The packing runs on a pool of
+ * MSM_HOST_PACK_THREADS (default 8) threads per device context, created on first use and parked
+ * between calls, plus three pinned staging buffers per context (up to 32 MiB each at 2^20).  The
+ * caller keeps ownership of the arrays; they are not read after the call returns. */
 int msm_compute(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, const msm_opts* opts,
                 uint32_t out_xy_be[16]);
 
