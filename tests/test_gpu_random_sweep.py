@@ -1,4 +1,5 @@
-"""Seeded random sweep of libmsm's entry points: sizes from 1 to 2^19 (log-uniform, ragged),
+"""Seeded random sweep of libmsm's entry points: sizes from 1 to 2^19 (log-uniform, ragged; the
+MSM_SWEEP_* variables below run other seeds, counts and sizes),
 explicit or automatic window widths 4..20, run lengths, host / device / pipelined / shared-base
 entries, batch counts and split partials, every result bit-exact against the closed form
 sum s_i (k_i G) = ((sum s_i k_i) mod r) G over P_i = (k0 + i step) G (tests/_closed_form.py; pinned to the Aleo-wasm oracle
@@ -13,15 +14,19 @@ from _closed_form import as_xy, closed_form
 
 pytestmark = pytest.mark.gpu
 
-SEED = 20261016
-N_CASES = 120
+import os
+
+# MSM_SWEEP_SEED / MSM_SWEEP_CASES run a different or longer sweep (profiles/r5/random_sweep_*.txt)
+SEED = int(os.environ.get("MSM_SWEEP_SEED", "20261016"))
+N_CASES = int(os.environ.get("MSM_SWEEP_CASES", "120"))
+MAX_LOG = int(os.environ.get("MSM_SWEEP_MAXLOG", "19"))  # sizes up to 2^MAX_LOG
 
 
 def _cases():
     rng = np.random.default_rng(SEED)
     out = []
     for i in range(N_CASES):
-        n = int(np.exp(rng.uniform(0, np.log(1 << 19))))
+        n = int(np.exp(rng.uniform(0, np.log(1 << MAX_LOG))))
         window = int(rng.choice([0, 0, 4, 7, 9, 11, 13, 14, 15, 16, 17, 20]))
         if window and n > (1 << 17) and window < 9:
             window = 0  # keep the number of narrow windows (and the runtime) bounded
