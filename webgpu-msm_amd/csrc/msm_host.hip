@@ -322,26 +322,29 @@ int get_ctx(int device, DevCtx** out) {
     bool ok = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) == hipSuccess;
     for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) == hipSuccess;
     for (Slot& sl : c->slot) ok = ok && hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking) == hipSuccess;
-    if (!ok) {
+    auto ev = [&](hipEvent_t* e, bool timed) {
+      ok = ok && (timed ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming)) == hipSuccess;
+    };
+    for (int i = 0; i < PH_COUNT; i++) ev(&c->ev[i], true);
+    for (int i = 0; i < NCHUNK_EV; i++) ev(&c->ev_chunk[i], false);
+    ev(&c->ev_user, false);
+    ev(&c->ev_shared, false);
+    ev(&c->ev_base, true);
+    for (Slot& sl : c->slot) {
+      ev(&sl.ev_start, true);
+      ev(&sl.ev_acc0, true);
+      ev(&sl.ev_acc1, true);
+      ev(&sl.ev_end, true);
+      ev(&sl.ev_done, false);
+      ev(&sl.ev_in, false);
+      ev(&sl.ev_sc, false);
+      ev(&sl.ev_fork, false);
+      ev(&sl.ev_join, false);
+    }
+    if (!ok) {  // no context without its streams and events (a null event would fail every call later)
       delete c;
       hipSetDevice(prev);
       return MSM_ERR_HIP;
-    }
-    for (int i = 0; i < PH_COUNT; i++) hipEventCreate(&c->ev[i]);
-    for (int i = 0; i < NCHUNK_EV; i++) hipEventCreateWithFlags(&c->ev_chunk[i], hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_user, hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_shared, hipEventDisableTiming);
-    hipEventCreate(&c->ev_base);
-    for (Slot& sl : c->slot) {
-      hipEventCreate(&sl.ev_start);
-      hipEventCreate(&sl.ev_acc0);
-      hipEventCreate(&sl.ev_acc1);
-      hipEventCreate(&sl.ev_end);
-      hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming);
-      hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming);
-      hipEventCreateWithFlags(&sl.ev_sc, hipEventDisableTiming);
-      hipEventCreateWithFlags(&sl.ev_fork, hipEventDisableTiming);
-      hipEventCreateWithFlags(&sl.ev_join, hipEventDisableTiming);
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1467,12 +1470,6 @@ int launch_parts(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Bat
   return MSM_OK;
 }
 
-// Make the slot's stream wait for its inputs: uploads on the copy stream and/or the caller's
-// stream (recorded into ev_in / ev_user beforehand).
-int wait_event(hipStream_t s, hipEvent_t e) {
-  HIPCHECK(hipStreamWaitEvent(s, e, 0));
-  return MSM_OK;
-}
 
 // Wait for the launch in slot `si` (spinning briefly: the result is usually due within a couple of
 // milliseconds, and a blocking wait adds a wake-up latency) and check its flags; its window terms
