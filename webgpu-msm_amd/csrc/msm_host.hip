@@ -1711,6 +1711,11 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
     // packed (as the split, §2.6): the scalars through the pinned ring, then each 8 MiB piece of
     // points as x|y (x|y|z for a piece with some z != 1), prepared in its own format as it lands
     if (!c->packer) c->packer = new PackPool(pack_threads());
+    // the ring at its size before anything is enqueued (a growth bumps the allocation generation)
+    for (int r = 0; r < NPIN; r++) {
+      void* b;
+      if ((rc = pin_take(c, r, std::min(n, UPLOAD_PTS_PIECE) * 96, &b)) != MSM_OK) return rc;
+    }
     int k = 0;
     uint32_t* wsc = w.wire_sc.as<uint32_t>();
     for (size_t off = 0; off < n; off += UPLOAD_PTS_PIECE, k++) {
