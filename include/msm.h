@@ -208,7 +208,8 @@ int msm_compute_shared_device(const uint32_t* d_points_be, const uint32_t* const
  * independent MSMs, per-MSM host arrays; msm_compute_shared: one host base vector, per-MSM host
  * scalar vectors.  Inputs are uploaded on a copy stream into the in-flight launch slots while the
  * other slots compute (the base vector of msm_compute_shared once, piece by piece, prepared as it
- * lands).  Results [count][16]. */
+ * lands); msm_compute_many packs x|y of every point as msm_compute does (t checked on the host,
+ * MSM_ERR_COORD_RANGE for t >= p).  Results [count][16]. */
 int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
                      const msm_opts* opts, uint32_t* out_xy_be);
 int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,

@@ -156,6 +156,8 @@ for step in "$@"; do
       run e2etrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
         -d gpurun_out/${TAG}_e2etrace_d -o run -- python3 tools/e2e_probe.py --runs 8 ;;
     e2e) run e2e 120 python tools/e2e_probe.py --runs 12 ;;
+    manyhost:*)  # manyhost:NAME -- msm_compute_many from host arrays (16 x 2^18), under the current set: knobs
+      run "manyhost_${step#manyhost:}" 300 python tools/many_host_probe.py ;;
     e2esz:*)  # e2esz:NAME:SIZES -- tools/e2e_size_probe.py over the listed sizes (under the current set: knobs)
       IFS=: read -r _ nm sz <<< "$step"
       run "e2esz_$nm" 300 python tools/e2e_size_probe.py --sizes "$sz" --runs 7 --rounds 1 ;;

@@ -1823,7 +1823,8 @@ struct ManyInputs {
                                                 // uploaded into instead of the slot's wire buffer
   bool packed = false;  // host points packed by the library's threads into pinned staging (x|y, or
                         // x|y|z for a launch with some z != 1) and copied into dev_points (24 words
-                        // of room per point); the launch's k_prepare_points reads that format
+                        // of room per point) or the slots' wire buffers; the launch's
+                        // k_prepare_points reads that format
   const uint32_t* const* dev_scalars = nullptr;  // host inputs whose scalars are already on the
                                                  // device (n + padding words per MSM): no scalar upload
 };
@@ -1927,10 +1928,18 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // copy per array: each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between
   // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
   // up alone and its tail is padded on the device.
-  const bool packed = host && in.packed && in.dev_points && !shared;
+  const bool packed = host && in.packed && !shared;
   std::vector<uint32_t> launch_fmt(nbatch, PT_FMT_WIRE);  // the packed launches' point formats
   std::atomic<bool> t_bad{false};                         // a packed t >= p (MSM_ERR_COORD_RANGE)
-  if (packed && !c->packer) c->packer = new PackPool(pack_threads());
+  if (packed) {
+    if (!c->packer) c->packer = new PackPool(pack_threads());
+    // the staging ring at its size before anything is enqueued (a growth bumps the allocation
+    // generation)
+    for (int k = 0; k < NPIN; k++) {
+      void* b;
+      if ((rc = pin_take(c, k, (size_t)nm * n * 128, &b)) != MSM_OK) return fail0(rc);
+    }
+  }
   auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
@@ -2820,6 +2829,7 @@ int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* sc
   in.kind = ManyInputs::HOST;
   in.points = points_be;
   in.scalars = scalars_be;
+  in.packed = host_pack();  // x|y (x|y|z) through the pinned ring into the slots' wire buffers
   return multi_many_entry(in, n, count, opts, nullptr, out_xy_be, false);
 }
 
