@@ -113,13 +113,18 @@ def test_t_is_checked_but_not_used(n):
         bad_t[i, 16:24] = np.uint32(0x01234567) ^ np.arange(8, dtype=np.uint32)  # t < p, not x y
     assert M.compute_msm_wire(bad_t, sc) == exp
     assert M.compute_msm_device(_dev(bad_t), _dev(sc), n) == exp
+    # the host batch API packs the same way: three MSMs in one call, the bad t in the second
+    many = M.compute_msm_many([pts, bad_t, pts], [sc, sc, sc], n)
+    assert all(tuple(as_xy(r)) == tuple(exp) for r in many)
     over = pts.copy()
     over[n - 2, 16:24] = 0xFFFFFFFF  # t >= p
-    for fn in (lambda: M.compute_msm_wire(over, sc), lambda: M.compute_msm_device(_dev(over), _dev(sc), n)):
+    for fn in (lambda: M.compute_msm_wire(over, sc), lambda: M.compute_msm_device(_dev(over), _dev(sc), n),
+               lambda: M.compute_msm_many([pts, over, pts], [sc, sc, sc], n)):
         with pytest.raises(M.MsmError) as e:
             fn()
         assert e.value.code == -3
     assert M.compute_msm_wire(pts, sc) == exp  # recovers
+    assert tuple(as_xy(M.compute_msm_many([pts], [sc], n)[0])) == tuple(exp)
 
 
 def test_host_many_distinct():
