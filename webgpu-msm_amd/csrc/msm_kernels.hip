@@ -340,7 +340,10 @@ constexpr uint32_t PS_R = MSM_PS_R;  // digits per lane (ch = PT_THREADS * PS_R)
 #define MSM_RC_THREADS 1024
 #endif
 constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
-constexpr uint32_t RC_SPAN = 4096;  // scalars per recode workgroup
+#ifndef MSM_RC_SPAN
+#define MSM_RC_SPAN 4096
+#endif
+constexpr uint32_t RC_SPAN = MSM_RC_SPAN;  // scalars per recode workgroup
 template <typename T>
 // blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its windows
 // [y Wr, (y+1) Wr).  Every window is recoded (the carries climb through them all); only the
