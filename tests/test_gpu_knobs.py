@@ -57,6 +57,7 @@ print(json.dumps(out))
     {"MSM_RED2_TREE": "0"},                        # k_bucket_reduce_2 for the second stage
     {"MSM_HORNER_THREADS": "0", "MSM_FORK_PREP_PIPE": "1"},  # tails inline, preparation forked
     {"MSM_HOST_SORT_EARLY": "0", "MSM_HOST_PACK_THREADS": "1"},
+    {"MSM_PIN_MAX_MB": "1"},                       # staging ring over its cap: every entry unpacked
 ])
 def test_knob_paths_bit_exact(env):
     e = dict(os.environ)

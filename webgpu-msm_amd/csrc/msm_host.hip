@@ -1198,6 +1198,26 @@ int pin_give(DevCtx* c, int k, hipStream_t s) {
   return MSM_OK;
 }
 
+// Every staging buffer of the ring at `bytes` before a packed call enqueues anything (a growth
+// bumps the allocation generation).  False -- the call then uploads unpacked -- for buffers over
+// 512 MiB (a launch of more than ~2^22 points: that much pinned memory per buffer costs more to
+// allocate than packing saves) or when the pinned allocation fails.
+size_t pin_max_bytes() {  // MSM_PIN_MAX_MB overrides (tests force the fallback with a small cap)
+  static const size_t v = getenv("MSM_PIN_MAX_MB") ? (size_t)atol(getenv("MSM_PIN_MAX_MB")) << 20 : size_t(512) << 20;
+  return v;
+}
+bool pin_ring_ready(DevCtx* c, size_t bytes) {
+  if (bytes > pin_max_bytes()) return false;
+  for (int k = 0; k < NPIN; k++) {
+    void* b;
+    if (pin_take(c, k, bytes, &b) != MSM_OK) {
+      (void)hipGetLastError();
+      return false;
+    }
+  }
+  return true;
+}
+
 // Worker threads of the pool (MSM_HORNER_THREADS; 0 = the launching thread runs the tails itself).
 int horner_threads() {
   static const int v =
@@ -1707,15 +1727,10 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   };
   bool t_bad = false;  // some t >= p, checked on the host (t is not uploaded): reported once the
                        // MSM has run, so the device's flags end cleared as after any call
-  if (host_pack()) {
+  if (host_pack() && pin_ring_ready(c, std::min(n, UPLOAD_PTS_PIECE) * 96)) {
     // packed (as the split, §2.6): the scalars through the pinned ring, then each 8 MiB piece of
     // points as x|y (x|y|z for a piece with some z != 1), prepared in its own format as it lands
     if (!c->packer) c->packer = new PackPool(pack_threads());
-    // the ring at its size before anything is enqueued (a growth bumps the allocation generation)
-    for (int r = 0; r < NPIN; r++) {
-      void* b;
-      if ((rc = pin_take(c, r, std::min(n, UPLOAD_PTS_PIECE) * 96, &b)) != MSM_OK) return rc;
-    }
     int k = 0;
     uint32_t* wsc = w.wire_sc.as<uint32_t>();
     for (size_t off = 0; off < n; off += UPLOAD_PTS_PIECE, k++) {
@@ -1928,18 +1943,10 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // copy per array: each pageable hipMemcpyAsync costs ~20 us of copy-engine idle time between
   // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
   // up alone and its tail is padded on the device.
-  const bool packed = host && in.packed && !shared;
+  const bool packed = host && in.packed && !shared && pin_ring_ready(c, (size_t)nm * n * 128);
   std::vector<uint32_t> launch_fmt(nbatch, PT_FMT_WIRE);  // the packed launches' point formats
   std::atomic<bool> t_bad{false};                         // a packed t >= p (MSM_ERR_COORD_RANGE)
-  if (packed) {
-    if (!c->packer) c->packer = new PackPool(pack_threads());
-    // the staging ring at its size before anything is enqueued (a growth bumps the allocation
-    // generation)
-    for (int k = 0; k < NPIN; k++) {
-      void* b;
-      if ((rc = pin_take(c, k, (size_t)nm * n * 128, &b)) != MSM_OK) return fail0(rc);
-    }
-  }
+  if (packed && !c->packer) c->packer = new PackPool(pack_threads());
   auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
@@ -2293,18 +2300,13 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   in.batch = nmb;
   in.lens = lens.data();
   std::vector<const uint32_t*> dsc(G);
-  const bool pack = host_scalars_first() && host_own_points() && host_pack();
+  const bool pack =
+      host_scalars_first() && host_own_points() && host_pack() && pin_ring_ready(c, (size_t)nmb * s * 128);
   if (pack) {
     // packed: every launch's scalars and points go up through the pinned ring from the uploader,
     // scalars first (run_many), into these device regions (slice g at g s)
     if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
     if (!c->packer) c->packer = new PackPool(pack_threads());
-    // every staging buffer at its size before anything is enqueued: a later growth would bump
-    // the allocation generation mid-call
-    for (int k = 0; k < NPIN; k++) {
-      void* b;
-      if (int rc = pin_take(c, k, (size_t)nmb * s * 128, &b)) return rc;
-    }
     for (size_t g = 0; g < G; g++) dsc[g] = c->host_sc.as<uint32_t>() + g * s * 8;
     in.dev_scalars = dsc.data();
   } else if (host_scalars_first()) {
