@@ -1203,7 +1203,8 @@ int pin_give(DevCtx* c, int k, hipStream_t s) {
 // 512 MiB (a launch of more than ~2^22 points: that much pinned memory per buffer costs more to
 // allocate than packing saves) or when the pinned allocation fails.
 size_t pin_max_bytes() {  // MSM_PIN_MAX_MB overrides (tests force the fallback with a small cap)
-  static const size_t v = getenv("MSM_PIN_MAX_MB") ? (size_t)atol(getenv("MSM_PIN_MAX_MB")) << 20 : size_t(512) << 20;
+  static const long mb = getenv("MSM_PIN_MAX_MB") ? atol(getenv("MSM_PIN_MAX_MB")) : 512;
+  static const size_t v = mb >= 0 && mb < (1l << 30) ? (size_t)mb << 20 : size_t(512) << 20;
   return v;
 }
 bool pin_ring_ready(DevCtx* c, size_t bytes) {
@@ -2225,7 +2226,8 @@ int on_device(const msm_opts* opts, F&& fn) {
 
 // Host-input points per slice of a split MSM (run_host_split), and MSMs per launch there.
 size_t host_piece() {
-  static const size_t v = getenv("MSM_HOST_PIECE_LOG") ? (size_t)1 << atoi(getenv("MSM_HOST_PIECE_LOG")) : (size_t)1 << 17;
+  static const int lg = getenv("MSM_HOST_PIECE_LOG") ? atoi(getenv("MSM_HOST_PIECE_LOG")) : 17;
+  static const size_t v = (size_t)1 << (lg >= 10 && lg <= 24 ? lg : 17);
   return v;
 }
 uint32_t host_batch() {  // two slices per launch: measured best for 2^17 slices
@@ -2252,8 +2254,8 @@ bool host_scalars_first() {
 // such tails slower (one more launch, and the copies waited for slots); re-measured with the
 // call's own upload buffers.
 size_t host_tail() {
-  static const size_t v = getenv("MSM_HOST_TAIL_LOG") && atoi(getenv("MSM_HOST_TAIL_LOG")) > 0
-                              ? (size_t)1 << atoi(getenv("MSM_HOST_TAIL_LOG")) : 0;
+  static const int lg = getenv("MSM_HOST_TAIL_LOG") ? atoi(getenv("MSM_HOST_TAIL_LOG")) : 0;
+  static const size_t v = lg > 0 && lg <= 24 ? (size_t)1 << lg : 0;
   return v;
 }
 
