@@ -145,9 +145,10 @@ for step in "$@"; do
     kstats1lib:*)
       IFS=: read -r _ libs <<< "$step"
       for lib in ${libs//,/ }; do
+        # shellcheck disable=SC2086
         MSM_SLOTS=1 MSM_FORK_PREP=0 MSM_AMD_LIB=$LIBDIR/$lib run "kstats1_${lib%.so}${KS:-}" 300 rocprofv3 --kernel-trace \
           --stats --output-format csv -d "gpurun_out/${TAG}_kstats1_${lib%.so}${KS:-}_d" -o run -- python3 bench.py --no-extras \
-          "${BENCH_Q[@]}" --steps 40 --warmup 10
+          "${BENCH_Q[@]}" --steps 40 --warmup 10 ${BENCH_X:-}
       done ;;
     latprof)
       run latprof 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_latprof_d -o run \
