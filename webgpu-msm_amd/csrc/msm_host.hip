@@ -4,9 +4,10 @@
 //   compute_msm            src/submission/submission.ts:25-157   -> msm_compute / msm_compute_device
 //   getBestWindowSize      submission.ts:18-23                    -> msm_best_window
 //   gpuIntraBucketReduction src/submission/gpu.ts:36-285          -> k_prepare_points .. k_lead_scan
-//     (its staging ring, gpu.ts:146-155 / 244-271)                -> upload_points (chunked, overlapped)
+//     (its staging ring, gpu.ts:146-155 / 244-271)                -> the packed pinned ring (PinRing,
+//                                                                    PackPool) and the uploader thread
 //   split_dynamic          msm-wasm/src/lib.rs:196-202            -> msm_split (host) / k_recode_* (device)
-//   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1/2
+//   inter_bucket_reduce    lib.rs:46-56, 123-133                  -> k_bucket_reduce_1, k_red2_groups / _terms
 //   reduce_last            lib.rs:88-104                          -> horner_tail (host)
 //   point_add_affine       lib.rs:240-253                         -> msm_point_add_affine
 //   msm_end_to_end         lib.rs:24-44, 106-121                  -> msm_compute_cpu (msm_cpu.h)

@@ -18,8 +18,12 @@
 //                      (segmented scan for long chains)
 //   k_lead_scan        chains bucket continuations that run through whole workgroups (skew only)
 //   k_bucket_reduce_1  per (window, chunk of L buckets): running sums -> U_c = sum (i+1) B, T_c = sum B
-//   k_bucket_reduce_2  per (window, term): plain sums R_{w,V} = sum_c U_c, R_{w,k} = sum_{c: bit k} T_c,
-//                      converted to canonical standard form for the host Horner
+//   k_red2_groups      per (window, group of 128 chunks): V_g = sum U_c, S_g = sum T_c and the
+//                      group's low bit terms R_{g,k}, in LDS (quad-cooperative adds)
+//   k_red2_terms       per (window, term): R_{w,V} = sum V_g, R_{w,k} = sum_g R_{g,k} or
+//                      sum_{g: bit k-7} S_g, in the host's Montgomery form for the host Horner
+//   k_bucket_reduce_2  the same terms straight from every chunk's U_c / T_c (windows of more than
+//                      64 groups, or MSM_RED2_TREE=0)
 //
 // Digit semantics differ from the reference's (unsigned, MSB-first, lib.rs:58-84 + msm-macro) on
 // purpose: only the final affine (x, y) is the parity contract, and signed digits halve the
