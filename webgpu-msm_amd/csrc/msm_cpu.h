@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include "msm_util.h"
+
 #include "hostfield.h"
 
 namespace msmh {
@@ -100,24 +102,6 @@ static inline int cpu_prepare(const uint32_t* pts_be, size_t lo, size_t hi, PreA
     }
   }
   return MSM_OK;
-}
-
-// Threads the host can run at once: the hardware threads, capped by a cgroup-v2 CPU quota
-// (/sys/fs/cgroup/cpu.max = "quota period"): a container reports the whole machine's threads
-// (256 on an MI355X node) while its quota may allow 16, and 256 threads on 16 CPUs thrash.
-static inline unsigned host_threads() {
-  static const unsigned t = [] {
-    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-      char quota[32] = {0};
-      unsigned long long period = 0;
-      if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0)
-        hw = (unsigned)std::min<unsigned long long>(hw, std::max(1ull, strtoull(quota, nullptr, 10) / period));
-      fclose(f);
-    }
-    return hw;
-  }();
-  return t;
 }
 
 static inline int cpu_msm(const uint32_t* points_be, const uint32_t* scalars_be, size_t n, uint32_t c,

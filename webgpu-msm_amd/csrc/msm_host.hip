@@ -151,13 +151,13 @@ bool plan_eq(const Plan& a, const Plan& b) {
 // Device workspace of one MSM (all sizes from Plan; grown on demand, never shrunk).
 struct Workspace {
   Buf pts, err, digits, colsum, bin_base, bin_cur;
-  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets, big_tiles, cursor;
+  Buf part_entry, part_fine, sorted_entry, bucket_start, run_key, buckets;
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
   Buf wire_pts, wire_sc;  // device copies of host-resident inputs (msm_compute*, host entries)
   Buf red_G;               // k_red2_groups' points per (window, group of RG_CH chunks)
   void release() {
     Buf* bufs[] = {&pts, &err, &digits, &colsum, &bin_base, &bin_cur, &part_entry, &part_fine,
-                   &sorted_entry, &bucket_start, &run_key, &buckets, &big_tiles, &cursor, &lead_val, &lead_open, &cross_key,
+                   &sorted_entry, &bucket_start, &run_key, &buckets, &lead_val, &lead_open, &cross_key,
                    &lead_flag, &skew_list, &g_head, &g_hkey, &g_tkey, &red_U, &red_T, &wire_pts, &wire_sc, &red_G};
     for (Buf* b : bufs) b->release();
   }
@@ -567,7 +567,7 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(pts, (size_t)(d.shared ? 1 : d.nm) * d.n * PRE_WORDS * 4);
   ENS(err, 16);
   ENS(digits, (size_t)d.W * d.n * 4);
-  ENS(colsum, (size_t)d.nbins * 4);
+  ENS(colsum, ((size_t)d.nbins + d.W) * 4);  // bin totals, then window totals
   ENS(bin_base, ((size_t)d.nbins + 1) * 4);
   ENS(bin_cur, (size_t)d.nbins * 4);
   ENS(part_entry, pl.Mmax * 4);
@@ -575,8 +575,6 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(sorted_entry, pl.Mmax * 4 + 16);  // + a 16-B tail for k_accumulate's vector entry loads
   ENS(bucket_start, (nb + 2) * 4);
   ENS(run_key, pl.runs_max * 4);
-  ENS(big_tiles, (pl.Mmax / FS_CAP + d.nbins + 1) * 8 + 8);
-  ENS(cursor, nb * 4);
   ENS(buckets, nb * PT_WORDS * 4);
   const size_t nwg = pl.runs_max / ACC_THREADS + 2;
   ENS(lead_val, nwg * PT_WORDS * 4);
@@ -592,14 +590,15 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   if (red2_tree(pl)) ENS(red_G, (size_t)d.W * red2_groups(pl) * RG_OUT * PT_WORDS * 4);
 #undef ENS
   if (g_alloc_gen.load() != gen0) {
-    // err, lead_flag and colsum are kept all-zero between MSMs by the kernels themselves
-    // (k_bucket_reduce_2 clears the flags, k_bin_scan the bin totals it consumed), so a
+    // err, lead_flag, colsum and bin_cur are kept all-zero between MSMs by the kernels themselves
+    // (k_bucket_reduce_2 clears the flags, k_fine_sort the bin totals and cursors), so a
     // replayed graph needs no memset nodes; fresh allocations start that invariant here.
     hipStream_t st = sl0.stream;
     if (hipMemsetAsync(w.err.p, 0, w.err.cap, st) != hipSuccess ||
         hipMemsetAsync(w.lead_flag.p, 0, w.lead_flag.cap, st) != hipSuccess ||
         hipMemsetAsync(w.skew_list.p, 0, 4, st) != hipSuccess ||
-        hipMemsetAsync(w.colsum.p, 0, w.colsum.cap, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        hipMemsetAsync(w.colsum.p, 0, w.colsum.cap, st) != hipSuccess ||
+        hipMemsetAsync(w.bin_cur.p, 0, w.bin_cur.cap, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
       return MSM_ERR_HIP;
   }
   const size_t hbytes = (size_t)d.W * pl.nterms * 32 * 4 + 64;
@@ -647,6 +646,57 @@ void launch_prepare(const uint32_t* wire, uint32_t* pts_out, uint32_t cnt, uint3
                      err, nt, fmt);
 }
 
+// The scalar recoding: the fixed-geometry kernel for the common window widths (c = 13..16,
+// recode_fixed), the generic loop for the others (MSM_RECODE_FIXED=0 forces it everywhere).
+bool recode_fixed_on() {
+  static const bool on = !(getenv("MSM_RECODE_FIXED") && atoi(getenv("MSM_RECODE_FIXED")) == 0);
+  return on;
+}
+template <uint32_t Q, uint32_t NHI>
+void launch_recode_fixed(const MsmDims& d, const BatchPtrs& sc, void* digits, uint32_t* colsum, hipStream_t s) {
+  const bool full = d.w0 == 0 && d.Wr == d.Wm && !d.half_lo && !d.half_hi;
+  const dim3 grid(grid_for(d.n, RC_SPAN), d.nm);
+  const size_t lds = ((size_t)d.Wr * d.nbc + d.Wr) * 4;
+  if (full)
+    hipLaunchKernelGGL((k_recode_fixed<Q, NHI, true>), grid, dim3(RC_THREADS), lds, s, sc, d,
+                       static_cast<uint16_t*>(digits), colsum);
+  else
+    hipLaunchKernelGGL((k_recode_fixed<Q, NHI, false>), grid, dim3(RC_THREADS), lds, s, sc, d,
+                       static_cast<uint16_t*>(digits), colsum);
+}
+void launch_recode(const MsmDims& d, const BatchPtrs& sc, void* digits, uint32_t* colsum, hipStream_t s) {
+  const dim3 grid(grid_for(d.n, RC_SPAN), d.nm);
+  const size_t lds = ((size_t)d.Wr * d.nbc + d.Wr) * 4;  // histogram + window totals
+  if (d.c > 16) {
+    hipLaunchKernelGGL(k_recode_hist<uint32_t>, grid, dim3(RC_THREADS), lds, s, sc, d, static_cast<uint32_t*>(digits),
+                       colsum);
+    return;
+  }
+  if (recode_fixed_on()) {
+    if (d.q == 15 && d.nhi == 14) return launch_recode_fixed<15, 14>(d, sc, digits, colsum, s);
+    if (d.q == 14 && d.nhi == 16) return launch_recode_fixed<14, 16>(d, sc, digits, colsum, s);
+    if (d.q == 13 && d.nhi == 7) return launch_recode_fixed<13, 7>(d, sc, digits, colsum, s);
+    if (d.q == 12 && d.nhi == 14) return launch_recode_fixed<12, 14>(d, sc, digits, colsum, s);
+  }
+  hipLaunchKernelGGL(k_recode_hist<uint16_t>, grid, dim3(RC_THREADS), lds, s, sc, d, static_cast<uint16_t*>(digits),
+                     colsum);
+}
+bool is_recode_kernel(const void* f) {
+  const void* ks[] = {reinterpret_cast<const void*>(&k_recode_hist<uint32_t>),
+                      reinterpret_cast<const void*>(&k_recode_hist<uint16_t>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<15, 14, true>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<15, 14, false>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<14, 16, true>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<14, 16, false>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<13, 7, true>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<13, 7, false>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<12, 14, true>),
+                      reinterpret_cast<const void*>(&k_recode_fixed<12, 14, false>)};
+  for (const void* k : ks)
+    if (f == k) return true;
+  return false;
+}
+
 // Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
 // h_out.  `pts` is the point-record buffer (the slot's own, or a shared base vector's).
 // With `acc_events` (eager launches only), k_accumulate runs between the slot's ev_acc0 / ev_acc1;
@@ -685,35 +735,25 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
       mark(PH_START);
       mark(PH_PREPARE);
     }
-    const size_t hist_lds = (size_t)d.Wr * d.nbc * 4;
-    const unsigned rc_grid = grid_for(d.n, RC_SPAN);
-    if (d.c <= 16) {
-      hipLaunchKernelGGL(k_recode_hist<uint16_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                         w.digits.as<uint16_t>(), w.colsum.as<uint32_t>());
-    } else {
-      hipLaunchKernelGGL(k_recode_hist<uint32_t>, dim3(rc_grid, d.nm), dim3(RC_THREADS), hist_lds, s, d_scalars, d,
-                         w.digits.as<uint32_t>(), w.colsum.as<uint32_t>());
-    }
+    launch_recode(d, d_scalars, w.digits.p, w.colsum.as<uint32_t>(), s);
     mark(PH_RECODE);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(BS_THREADS), 0, s, w.colsum.as<uint32_t>(),
-                       w.bin_base.as<uint32_t>(), w.bin_cur.as<uint32_t>(), d.nbins, w.big_tiles.as<uint32_t>());
     mark(PH_SCAN);
     if (d.c <= 16) {
-      hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 8, s,
-                         w.digits.as<uint16_t>(), d, w.bin_cur.as<uint32_t>(), w.part_entry.as<uint32_t>(),
+      hipLaunchKernelGGL(k_part_scatter<uint16_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                         w.digits.as<uint16_t>(), d, w.colsum.as<uint32_t>(), w.bin_cur.as<uint32_t>(),
+                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(),
                          w.part_fine.as<uint16_t>());
     } else {
-      hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 8, s,
-                         w.digits.as<uint32_t>(), d, w.bin_cur.as<uint32_t>(), w.part_entry.as<uint32_t>(),
+      hipLaunchKernelGGL(k_part_scatter<uint32_t>, dim3(d.nch, d.W), dim3(PT_THREADS), (size_t)d.nbc * 12, s,
+                         w.digits.as<uint32_t>(), d, w.colsum.as<uint32_t>(), w.bin_cur.as<uint32_t>(),
+                         w.bin_base.as<uint32_t>(), w.part_entry.as<uint32_t>(),
                          w.part_fine.as<uint16_t>());
     }
     mark(PH_SCATTER);
     hipLaunchKernelGGL(k_fine_sort, dim3(d.nbins), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
                        w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
-                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.cursor.as<uint32_t>());
-    hipLaunchKernelGGL(k_big_place, dim3(BP_GRID), dim3(FS_THREADS), 0, s, w.part_entry.as<uint32_t>(),
-                       w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, w.big_tiles.as<uint32_t>(),
-                       w.cursor.as<uint32_t>(), w.sorted_entry.as<uint32_t>());
+                       w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.colsum.as<uint32_t>(),
+                       w.bin_cur.as<uint32_t>());
     mark(PH_FINE);
   }
   if (fork) HIPCHECK(hipStreamWaitEvent(s, sl.ev_join, 0));
@@ -849,9 +889,24 @@ Pt horner_tail(const Plan& pl, const uint32_t* terms, uint32_t m = 0) {
 // MSM = sum_w 2^(off_w) W_w, taking each W_w as it becomes ready: ~254 doublings and ~W adds on the
 // critical path instead of ~254 doublings and ~W * nterms adds.  MSM_TAIL_THREADS sets the helper
 // count (default 3; 0 = the one-thread horner_tail).
+// The library's host threads are sized from the process's CPU budget (host_threads(): the
+// hardware threads capped by the cgroup quota -- 16 on the GPU boxes, whose nproc says 256), shared
+// among the devices of the running call (a device list runs one host thread per device, and each
+// device context keeps its own pools): per device b = max(2, budget / devices); packing threads
+// (the caller included) b / 2 up to 8, lone-MSM tail helpers b / 4 up to 3, pipelined-tail threads
+// b / 8 up to 2, plus one uploader during a host-array call.  At one device on a 16-CPU quota that
+// is the measured 8 / 3 / 2; a call over 8 devices gets 1 / 0 / 0 per device, so
+// its 7 device threads and 8 uploaders stay within the quota.  The MSM_*_THREADS variables fix a
+// count instead.
+thread_local int t_call_devices = 1;  // devices of the call running on this thread (for_each_device)
+int per_device_budget() { return std::max(2, (int)host_threads() / std::max(1, t_call_devices)); }
+int env_threads(const char* name, int lo, int hi) {
+  const char* e = getenv(name);
+  return e ? std::max(lo, std::min(hi, atoi(e))) : -1;
+}
 int tail_helpers() {
-  static const int v = getenv("MSM_TAIL_THREADS") ? std::max(0, std::min(16, atoi(getenv("MSM_TAIL_THREADS")))) : 3;
-  return v;
+  static const int env = env_threads("MSM_TAIL_THREADS", 0, 16);
+  return env >= 0 ? env : std::min(3, per_device_budget() / 4);
 }
 
 class TailCrew {
@@ -871,6 +926,7 @@ class TailCrew {
     for (std::thread& t : th_) t.join();
   }
   bool active() const { return !th_.empty(); }
+  int helpers() const { return (int)th_.size(); }
   void arm() {
     if (th_.empty()) return;
     wait_idle();  // the previous round is over (run() and disarm() wait for it too)
@@ -1028,6 +1084,7 @@ class HornerPool {
     }
     cv_.notify_one();
   }
+  int size() const { return (int)th_.size(); }
   // every job pushed so far has run
   void wait_all() {
     std::unique_lock<std::mutex> lk(mu_);
@@ -1061,7 +1118,8 @@ class HornerPool {
 };
 
 // The packed host upload's threads: run(fn) calls fn(k, K) on K threads (the caller is k = 0) and
-// returns when all are done.  Workers spin briefly between jobs, then sleep.
+// returns when all are done.  Workers sleep on a condition variable between jobs; the caller spins
+// (pausing) until they are done.
 class PackPool {
  public:
   explicit PackPool(int threads) : k_(std::max(1, threads)) {
@@ -1116,13 +1174,15 @@ class PackPool {
 // Whether run_host_split packs its points (MSM_HOST_PACK, default on): the library's threads copy
 // only x|y of every 128-B record (or x|y|z when some point of a launch has z != 1) into pinned
 // staging, and t is derived from x and y on the device -- half the PCIe bytes of the points.
+// pack_range uses AVX2 stores: a host without AVX2 uploads unpacked instead of faulting.
 bool host_pack() {
-  static const bool on = !(getenv("MSM_HOST_PACK") && atoi(getenv("MSM_HOST_PACK")) == 0);
+  static const bool on =
+      !(getenv("MSM_HOST_PACK") && atoi(getenv("MSM_HOST_PACK")) == 0) && __builtin_cpu_supports("avx2");
   return on;
 }
 int pack_threads() {
-  static const int v = getenv("MSM_HOST_PACK_THREADS") ? std::max(1, std::min(32, atoi(getenv("MSM_HOST_PACK_THREADS")))) : 8;
-  return v;
+  static const int env = env_threads("MSM_HOST_PACK_THREADS", 1, 32);
+  return env >= 0 ? env : std::max(1, std::min(8, per_device_budget() / 2));
 }
 
 // t < p for a coordinate in BE words (t is not uploaded by the packed path, so its range is
@@ -1222,9 +1282,53 @@ bool pin_ring_ready(DevCtx* c, size_t bytes) {
 
 // Worker threads of the pool (MSM_HORNER_THREADS; 0 = the launching thread runs the tails itself).
 int horner_threads() {
-  static const int v =
-      getenv("MSM_HORNER_THREADS") ? std::max(0, std::min(16, atoi(getenv("MSM_HORNER_THREADS")))) : 2;
-  return v;
+  static const int env = env_threads("MSM_HORNER_THREADS", 0, 16);
+  return env >= 0 ? env : std::min(2, per_device_budget() / 8);
+}
+
+// A device context's pools at the sizes above for the running call (re-created when the call's
+// share differs from the one they were made for; calls on a context hold its mutex).
+PackPool* ctx_packer(DevCtx* c) {
+  const int k = pack_threads();
+  if (!c->packer || c->packer->size() != k) {
+    delete c->packer;
+    c->packer = new PackPool(k);
+  }
+  return c->packer;
+}
+TailCrew* ctx_crew(DevCtx* c) {
+  const int h = tail_helpers();
+  if (!c->crew || c->crew->helpers() != h) {
+    delete c->crew;
+    c->crew = new TailCrew(h);
+  }
+  return c->crew;
+}
+// Pools the CPU test hooks start (msm_test_pack, msm_test_pools), stopped by msm_shutdown too.
+struct TestPools {
+  PackPool* packer = nullptr;
+  TailCrew* crew = nullptr;
+  HornerPool* pool = nullptr;
+  void stop() {
+    delete packer;
+    delete crew;
+    delete pool;
+    packer = nullptr;
+    crew = nullptr;
+    pool = nullptr;
+  }
+};
+std::mutex g_test_mu;
+TestPools g_test_pools;
+
+HornerPool* ctx_pool(DevCtx* c) {
+  const int h = horner_threads();
+  if (h == 0) return nullptr;
+  if (!c->pool || c->pool->size() != h) {
+    delete c->pool;
+    c->pool = new HornerPool(h);
+  }
+  return c->pool;
 }
 
 void pt_to_be_affine(const Pt& p, uint32_t out[16]) {
@@ -1332,8 +1436,6 @@ int find_input_nodes(Segment& sg) {
   std::vector<hipGraphNode_t> nodes(num);
   if (hipGraphGetNodes(sg.graph, nodes.data(), &num) != hipSuccess) return MSM_ERR_HIP;
   const void* f_prep = reinterpret_cast<const void*>(&k_prepare_points);
-  const void* f_rc16 = reinterpret_cast<const void*>(&k_recode_hist<uint16_t>);
-  const void* f_rc32 = reinterpret_cast<const void*>(&k_recode_hist<uint32_t>);
   for (hipGraphNode_t nd : nodes) {
     hipGraphNodeType ty;
     if (hipGraphNodeGetType(nd, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
@@ -1342,7 +1444,7 @@ int find_input_nodes(Segment& sg) {
     if (kp.func == f_prep) {
       sg.n_prep = nd;
       sg.p_prep = kp;
-    } else if (kp.func == f_rc16 || kp.func == f_rc32) {
+    } else if (is_recode_kernel(kp.func)) {
       sg.n_recode = nd;
       sg.p_recode = kp;
     }
@@ -1629,10 +1731,10 @@ int order_after_user(DevCtx* c, hipStream_t user, int nslot) {
 // The host tail of a lone MSM in slot `si`, over the device context's persistent helpers: armed
 // right after the launch (they spin while the device works), handed the terms when they land.
 int finish_lone(DevCtx* c, int si, Pt* result) {
-  if (!c->crew) c->crew = new TailCrew(tail_helpers());
-  c->crew->arm();
-  const int rc = finish_msm(c, si, result, nullptr, c->crew);
-  if (rc != MSM_OK) c->crew->disarm();  // no terms will come
+  TailCrew* crew = ctx_crew(c);
+  crew->arm();
+  const int rc = finish_msm(c, si, result, nullptr, crew);
+  if (rc != MSM_OK) crew->disarm();  // no terms will come
   return rc;
 }
 
@@ -1732,7 +1834,7 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   if (host_pack() && pin_ring_ready(c, std::min(n, UPLOAD_PTS_PIECE) * 96)) {
     // packed (as the split, §2.6): the scalars through the pinned ring, then each 8 MiB piece of
     // points as x|y (x|y|z for a piece with some z != 1), prepared in its own format as it lands
-    if (!c->packer) c->packer = new PackPool(pack_threads());
+    ctx_packer(c);
     int k = 0;
     uint32_t* wsc = w.wire_sc.as<uint32_t>();
     for (size_t off = 0; off < n; off += UPLOAD_PTS_PIECE, k++) {
@@ -1946,9 +2048,12 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // transfers.  The padding MSMs of a short last launch upload nothing; a short MSM (in.lens) goes
   // up alone and its tail is padded on the device.
   const bool packed = host && in.packed && !shared && pin_ring_ready(c, (size_t)nm * n * 128);
+  // run_host_split sized its own point buffers (in.dev_points) for packed records: no unpacked
+  // fallback into them (it checked the ring itself; only a failure since then lands here)
+  if (host && in.packed && !shared && !packed && in.dev_points) return MSM_ERR_HIP;
   std::vector<uint32_t> launch_fmt(nbatch, PT_FMT_WIRE);  // the packed launches' point formats
   std::atomic<bool> t_bad{false};                         // a packed t >= p (MSM_ERR_COORD_RANGE)
-  if (packed && !c->packer) c->packer = new PackPool(pack_threads());
+  if (packed) ctx_packer(c);
   auto upload_launch = [&](size_t j, const std::function<void()>& scalars_done) -> int {
     BatchPtrs bp, bs;
     const uint32_t nreal = launch_inputs(j, &bp, &bs);
@@ -2081,12 +2186,10 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
     if (up_th.joinable()) up_th.join();
   };
   // the device context's tail helpers take the last launch's host tails (armed once it is enqueued)
-  if (tail_helpers() > 0 && !c->crew) c->crew = new TailCrew(tail_helpers());
-  TailCrew* crew = tail_helpers() > 0 ? c->crew : nullptr;
+  TailCrew* crew = tail_helpers() > 0 ? ctx_crew(c) : nullptr;
   bool crew_armed = false;
   // and the pool the earlier launches' tails (their terms copied out per launch)
-  if (horner_threads() > 0 && !c->pool) c->pool = new HornerPool(horner_threads());
-  HornerPool* pool = horner_threads() > 0 ? c->pool : nullptr;
+  HornerPool* pool = ctx_pool(c);
   std::vector<std::vector<uint32_t>> launch_terms(pool ? nbatch : 0);
   auto fail = [&](int code) {
     if (crew_armed) crew->disarm();  // no terms will come
@@ -2277,10 +2380,17 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
   const uint32_t nmb = host_batch();
   size_t t = host_tail();
   if (t * nmb * 8 > n) t = 0;  // small MSMs: no tail launch
-  const size_t body = n - t * nmb;
-  size_t Gb = std::max<size_t>(1, std::min<size_t>(16, body / host_piece()));
-  Gb = (Gb + nmb - 1) / nmb * nmb;
-  const size_t s = (body + Gb - 1) / Gb;
+  size_t body, Gb, s;
+  for (;;) {
+    body = n - t * nmb;
+    Gb = std::max<size_t>(1, std::min<size_t>(16, body / host_piece()));
+    Gb = (Gb + nmb - 1) / nmb * nmb;
+    s = (body + Gb - 1) / Gb;
+    // every slice runs as an MSM of s points (run_many sizes its buffers and clamps lengths by s):
+    // a tail slice longer than a body slice would lose points, so then there is no tail launch
+    if (t <= s) break;
+    t = 0;
+  }
   std::vector<size_t> offs, lens;
   for (size_t g = 0; g < Gb; g++) {
     offs.push_back(std::min(g * s, body));
@@ -2309,7 +2419,7 @@ int run_host_split(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars
     // packed: every launch's scalars and points go up through the pinned ring from the uploader,
     // scalars first (run_many), into these device regions (slice g at g s)
     if (int rc = c->host_sc.ensure(G * s * 32)) return rc;
-    if (!c->packer) c->packer = new PackPool(pack_threads());
+    ctx_packer(c);
     for (size_t g = 0; g < G; g++) dsc[g] = c->host_sc.as<uint32_t>() + g * s * 8;
     in.dev_scalars = dsc.data();
   } else if (host_scalars_first()) {
@@ -2463,8 +2573,15 @@ template <typename F>
 int for_each_device(size_t D, F&& fn) {
   std::vector<int> rc(D, MSM_OK);
   std::vector<std::thread> th;
-  for (size_t i = 1; i < D; i++) th.emplace_back([&, i] { rc[i] = fn(i); });
+  for (size_t i = 1; i < D; i++)
+    th.emplace_back([&, i] {
+      t_call_devices = (int)D;
+      rc[i] = fn(i);
+    });
+  const int own = t_call_devices;
+  t_call_devices = (int)D;
   rc[0] = fn(0);
+  t_call_devices = own;
   for (std::thread& t : th) t.join();
   for (int r : rc)
     if (r != MSM_OK) return r;
@@ -2681,6 +2798,8 @@ void msm_shutdown(void) {
     delete c;
     c = nullptr;
   }
+  std::lock_guard<std::mutex> lk3(g_test_mu);
+  g_test_pools.stop();
 }
 
 int msm_device_count(void) {
@@ -3127,12 +3246,46 @@ int msm_test_plan(size_t n, uint32_t nm, int pipelined, const msm_opts* opts, ui
 // The host packing of the packed uploads (pack_records over a pool of MSM_HOST_PACK_THREADS):
 // n wire records -> out (16 words per point for fmt 1 = x|y, 24 for fmt 2 = x|y|z); *all_z_one =
 // whether every z is 1, *t_bad = whether some t >= p.  Host code only (no device needed).
+// The host thread pools a call over `ndev` devices runs per device context (CPU test hook,
+// no device needed): out[0] the CPU budget (host_threads: hardware threads capped by the cgroup
+// quota), out[1..3] packing threads (the caller included), lone-MSM tail helpers and pipelined-tail
+// threads per device, out[4] the threads the library adds for the whole call -- per device its
+// packing workers, helpers, tail threads and one uploader, plus a host thread per device but the
+// first.  With `run` the three pools are started at those sizes (replacing the previous set), given
+// one job each, and left parked until the next call or msm_shutdown.
+int msm_test_pools(int ndev, int run, int* out) {
+  if (ndev < 1 || ndev > 64 || !out) return MSM_ERR_INVALID_ARG;
+  const int own = t_call_devices;
+  t_call_devices = ndev;
+  const int pk = pack_threads(), th = tail_helpers(), hn = horner_threads();
+  t_call_devices = own;
+  out[0] = (int)host_threads();
+  out[1] = pk;
+  out[2] = th;
+  out[3] = hn;
+  out[4] = ndev * ((pk - 1) + th + hn + 1) + (ndev - 1);
+  if (!run) return MSM_OK;
+  std::lock_guard<std::mutex> lk(g_test_mu);
+  g_test_pools.stop();
+  g_test_pools.packer = new PackPool(pk);
+  g_test_pools.crew = new TailCrew(th);
+  g_test_pools.pool = hn ? new HornerPool(hn) : nullptr;
+  std::atomic<int> hits{0};
+  g_test_pools.packer->run([&](int, int) { hits.fetch_add(1); });
+  if (g_test_pools.pool) {
+    for (int i = 0; i < 2 * hn; i++) g_test_pools.pool->push([&] { hits.fetch_add(1); });
+    g_test_pools.pool->wait_all();
+  }
+  g_test_pools.crew->arm();  // the helpers wake and spin, then go back to sleep
+  g_test_pools.crew->disarm();
+  return hits.load() == pk + 2 * hn ? MSM_OK : MSM_ERR_HIP;
+}
+
 int msm_test_pack(const uint32_t* wire, size_t n, uint32_t fmt, uint32_t* out, int* all_z_one, int* t_bad) {
   if ((!wire || !out) && n) return MSM_ERR_INVALID_ARG;
   if (fmt != PT_FMT_XY && fmt != PT_FMT_XYZ) return MSM_ERR_INVALID_ARG;
-  static std::mutex mu;
-  static PackPool* pool = nullptr;
-  std::lock_guard<std::mutex> lk(mu);
+  std::lock_guard<std::mutex> lk(g_test_mu);
+  PackPool*& pool = g_test_pools.packer;
   if (!pool) pool = new PackPool(pack_threads());
   const size_t bytes = n * pt_fmt_slots(fmt) * 16;
   void* tmp = aligned_alloc(64, (bytes + 63) / 64 * 64 + 64);  // the nontemporal stores want 32-B alignment
@@ -3199,5 +3352,20 @@ int msm_test_point_op(uint32_t op, const uint32_t* p, const uint32_t* q, uint32_
   hipFree(dout);
   return MSM_OK;
 }
+
+#ifdef MSM_PHASE_PROBE
+// Tuning builds only: writes the sort kernels' phase stamps of the last launch (g_probe) to `path`.
+int msm_test_probe_dump(const char* path) {
+  static std::vector<uint64_t> buf(sizeof(g_probe) / 8);
+  if (hipDeviceSynchronize() != hipSuccess) return MSM_ERR_HIP;
+  if (hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(g_probe), sizeof(g_probe), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return MSM_ERR_HIP;
+  FILE* f = fopen(path, "wb");
+  if (!f) return MSM_ERR_INVALID_ARG;
+  fwrite(buf.data(), 8, buf.size(), f);
+  fclose(f);
+  return MSM_OK;
+}
+#endif
 
 }  // extern "C"

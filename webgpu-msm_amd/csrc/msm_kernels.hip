@@ -8,11 +8,9 @@
 //   k_recode_hist      signed c-bit digits per scalar (window-carry recoding, |d| <= 2^(c-1)),
 //                      written window-major (= first sort level: one contiguous array per window),
 //                      with the coarse-bin totals (LDS histogram, flushed with global atomics)
-//   k_bin_scan         exclusive scan of the bin totals (one workgroup)
 //   k_part_scatter     digits -> coarse bins (each chunk reserves and writes one contiguous slice
 //                      per bin)
 //   k_fine_sort        per coarse bin: LDS counting sort by bucket -> (entry, bucket key) lists
-//   k_big_place        tile-parallel placement of bins too big for k_fine_sort (skew only)
 //   k_accumulate       fixed-length runs per lane over the sorted list (mixed adds), whole buckets
 //                      written directly, buckets cut by run boundaries joined through LDS
 //                      (segmented scan for long chains)
@@ -33,6 +31,30 @@
 
 
 namespace msm {
+
+// Phase probe (tuning builds only, -DMSM_PHASE_PROBE=1): thread 0 of each workgroup of the sort
+// kernels stamps the shader clock at its phase boundaries into g_probe[kernel][workgroup][slot]
+// (slots 8 and 9: the 100 MHz real-time clock at slots 0 and 7); msm_test_probe_dump writes the
+// last launch's stamps to a file (tools/phase_probe.py reads them).
+#ifdef MSM_PHASE_PROBE
+constexpr uint32_t PROBE_WG = 16384, PROBE_SLOTS = 10;
+__device__ uint64_t g_probe[4][PROBE_WG][PROBE_SLOTS];
+#define PROBE(k, wg, s)                                                                   \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (wg) < PROBE_WG) {                                           \
+      g_probe[k][wg][s] = __builtin_readcyclecounter();                                  \
+      if ((s) == 0 || (s) == 7) g_probe[k][wg][8 + ((s) == 7)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                    \
+  } while (0)
+#define PROBE_WAIT_VM() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define PROBE(k, wg, s) \
+  do {                  \
+  } while (0)
+#define PROBE_WAIT_VM() \
+  do {                  \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // point preparation
@@ -278,39 +300,92 @@ __device__ __forceinline__ void load_scalar(const uint32_t* __restrict__ scalars
   load_be_words(scalars + (size_t)i * 8, s);
 }
 
-// Wave-level exclusive scan of one u32 per lane (64 lanes); returns the exclusive prefix and sets
-// `total` to the wave sum.
+// Wave-level inclusive scan of one u32 per lane (64 lanes, all active) by DPP: four row shifts
+// scan each 16-lane row, two row broadcasts carry the rows' totals across.  No LDS round trips
+// (the ds_bpermute form took ~0.5 us of latency per scan, a tenth of a k_fine_sort workgroup's life).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+// Exclusive scan of one u32 per lane; `total` = the wave sum.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t x = v;
-#pragma unroll
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  total = __shfl(x, 63, 64);
+  const uint32_t x = wave_incl_scan(v);
+  total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
 }
 
-// Exclusive scan of cnt[0..nf) in LDS by the first wave of the workgroup (nf <= 64 * per).
+// Exclusive scan of cnt[0..nf) in LDS by the first wave of the workgroup.  256 counters (the
+// scatter's bins, the wide fine sorts) go as one 16-B vector per lane and 128 as one 8-B vector;
+// other multiples of 256 as runs of vectors read twice (a register array would cost the calling
+// kernels their occupancy); other counts take the scalar loop.
 __device__ __forceinline__ void lds_excl_scan_wave0(uint32_t* cnt, uint32_t nf) {
-  if (threadIdx.x < 64) {
-    const uint32_t per = (nf + 63) / 64;
-    const uint32_t lo = threadIdx.x * per;
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  if (nf == 256) {
+    uint4* c4 = reinterpret_cast<uint4*>(cnt) + lane;
+    const uint4 v = *c4;
+    uint32_t tot;
+    const uint32_t run = wave_excl_scan(v.x + v.y + v.z + v.w, tot);
+    *c4 = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
+    return;
+  }
+  if ((nf & 255u) == 0) {
+    const uint32_t n4 = nf / 256;  // uint4s per lane
+    uint4* c4 = reinterpret_cast<uint4*>(cnt) + lane * n4;
     uint32_t local = 0;
-    for (uint32_t k = 0; k < per; k++)
-      if (lo + k < nf) local += cnt[lo + k];
+    for (uint32_t k = 0; k < n4; k++) {
+      const uint4 v = c4[k];
+      local += v.x + v.y + v.z + v.w;
+    }
     uint32_t tot;
     uint32_t run = wave_excl_scan(local, tot);
-    for (uint32_t k = 0; k < per; k++) {
-      if (lo + k < nf) {
-        const uint32_t c = cnt[lo + k];
-        cnt[lo + k] = run;
-        run += c;
-      }
+    for (uint32_t k = 0; k < n4; k++) {
+      const uint4 v = c4[k];
+      c4[k] = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
+      run += v.x + v.y + v.z + v.w;
+    }
+    return;
+  }
+  if (nf == 128) {
+    uint2* c2 = reinterpret_cast<uint2*>(cnt) + lane;
+    const uint2 v = *c2;
+    uint32_t tot;
+    const uint32_t run = wave_excl_scan(v.x + v.y, tot);
+    *c2 = make_uint2(run, run + v.x);
+    return;
+  }
+  const uint32_t per = (nf + 63) / 64;
+  const uint32_t lo = lane * per;
+  uint32_t local = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (lo + k < nf) local += cnt[lo + k];
+  uint32_t tot;
+  uint32_t run = wave_excl_scan(local, tot);
+  for (uint32_t k = 0; k < per; k++) {
+    if (lo + k < nf) {
+      const uint32_t c = cnt[lo + k];
+      cnt[lo + k] = run;
+      run += c;
     }
   }
 }
+
+// Fine bits of MSM window `wm`: every window keeps nbc coarse bins over its OWN buckets, so a
+// window narrower than the widest (the balanced 15-bit windows at c = 16, the 13-bit ones at
+// c = 14, the 3-bit overflow window) sorts fb - (c - b) fine bits per bin and its bins are as full
+// as the others'.  (With one fb for all, half of such a window's bins held all its entries --
+// 8,192 per bin at 2^20, past k_fine_sort's LDS staging -- and took the slow unstaged path.)
+__device__ __forceinline__ uint32_t win_fb(const MsmDims& d, uint32_t wm) {
+  const uint32_t drop = d.c - win_bits(d, wm);
+  return d.fb > drop ? d.fb - drop : 0u;
+}
+// The same for window w of a launch's batch (w in [0, W): MSM w / Wr, local window w % Wr).
+__device__ __forceinline__ uint32_t batch_win_fb(const MsmDims& d, uint32_t w) { return win_fb(d, d.w0 + w % d.Wr); }
 
 // Digit codes, window-major digits[w][i]: bucket b = |d| - 1 plus a sign bit, or ZERO.
 //   c <= 16: uint16_t, sign = bit 15, ZERO = 0xffff (b = 0x7fff with the sign set would be
@@ -330,7 +405,7 @@ struct DigitCode<uint32_t> {
 // Pass 0+1 (fused): each workgroup recodes RC_SPAN scalars into window-major digit codes (the
 // window-major layout is the first sort level for free: each window is one contiguous array) and
 // builds, in LDS, their histogram over every window's nbc coarse bins, flushed with global
-// atomics into the bin totals colsum[w][bin] (kept zeroed between MSMs by k_bin_scan).  Digits
+// atomics into the bin totals colsum[w][bin] (kept zeroed between MSMs by k_fine_sort).  Digits
 // are read back only once, by k_part_scatter.
 #ifndef MSM_PT_THREADS
 #define MSM_PT_THREADS 1024
@@ -348,10 +423,68 @@ constexpr uint32_t RC_THREADS = MSM_RC_THREADS;
 #define MSM_RC_SPAN 4096
 #endif
 constexpr uint32_t RC_SPAN = MSM_RC_SPAN;  // scalars per recode workgroup
+// Signed recoding with the window geometry fixed at compile time (the common widths: q = 15,
+// nhi = 14 is c = 16; 14/16 c = 15; 13/7 c = 14; 12/14 c = 13).  Adding the constant
+// C = sum_w (2^(b_w - 1) - 1) 2^off_w to the scalar makes every window independent: digit_w =
+// bits_w(s + C) - (2^(b_w - 1) - 1) is exactly the carry recoding of `recode` (a window's bits plus
+// the carry v give v when v <= 2^(b-1), else v - 2^b with a carry out -- the same as
+// (v + 2^(b-1) - 1) mod 2^b - (2^(b-1) - 1) and the add's own carry), and the overflow window is
+// t's bits 254 and up, the add's carry out included (<= 4, never negative).  So each window is one
+// funnel shift of two known words and a mask: no 256-bit shift per window and no per-window scalar
+// bookkeeping (the generic loop issued more scalar than vector instructions).
+template <uint32_t Q, uint32_t NHI>
+struct FixedGeo {
+  static constexpr uint32_t WMAIN = (MAIN_BITS - NHI) / Q;
+  static constexpr uint32_t bits(uint32_t w) { return w < NHI ? Q + 1 : Q; }
+  static constexpr uint32_t off(uint32_t w) { return w * Q + (w < NHI ? w : NHI); }
+  struct Words {
+    uint32_t v[8];
+  };
+  static constexpr Words bias() {
+    Words c{};
+    for (uint32_t w = 0; w < WMAIN; w++) {
+      const uint64_t h = (1ull << (bits(w) - 1)) - 1ull;  // < 2^16, spans at most two words
+      const uint32_t o = off(w), k = o / 32, sh = o % 32;
+      const uint64_t lo = (uint64_t)c.v[k] + ((h << sh) & 0xffffffffull);
+      c.v[k] = (uint32_t)lo;
+      uint64_t carry = (lo >> 32) + ((h << sh) >> 32);
+      for (uint32_t j = k + 1; j < 8 && carry; j++) {
+        const uint64_t x = (uint64_t)c.v[j] + carry;
+        c.v[j] = (uint32_t)x;
+        carry = x >> 32;
+      }
+    }
+    return c;
+  }
+};
+
+// The recode's LDS histogram [Wr][nbc] into the bin totals colsum[w][bin] (global atomics), and
+// the windows' totals (LDS words after the histogram, summed per wave when a wave's 64 bins lie in
+// one window) into wtot[w] = colsum[nbins + w]: k_part_scatter takes a window's first slot from
+// the totals of the windows below it.  colsum and wtot are zeroed again by k_fine_sort.
+__device__ __forceinline__ void flush_hist(uint32_t* lds_hist, const MsmDims& d, uint32_t w0,
+                                           uint32_t* __restrict__ colsum) {
+  const uint32_t nh = d.Wr * d.nbc, lg = __builtin_ctz(d.nbc);
+  uint32_t* wt = lds_hist + nh;
+  for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) {
+    const uint32_t v = lds_hist[b];
+    if (v) atomicAdd(&colsum[w0 * d.nbc + b], v);
+    if (d.nbc >= 64) {
+      const uint32_t t = wave_incl_scan(v);
+      if ((threadIdx.x & 63) == 63 && t) atomicAdd(&wt[b >> lg], t);
+    } else if (v) {
+      atomicAdd(&wt[b >> lg], v);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < d.Wr && wt[threadIdx.x]) atomicAdd(&colsum[d.nbins + w0 + threadIdx.x], wt[threadIdx.x]);
+}
+
+// Pass 0+1 (fused), blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its
+// windows [y Wr, (y+1) Wr).  Carries only climb, so windows below the launch's range [d.w0, d.w0 +
+// d.Wr) are recoded for their carries (the generic loop stops at the range's top); only the range
+// is written and counted.  The generic form (`recode`) serves any geometry.
 template <typename T>
-// blockIdx.y = MSM of the batch: scalars from scalar_sets.p[y], digits into its windows
-// [y Wr, (y+1) Wr).  Every window is recoded (the carries climb through them all); only the
-// launch's window range [d.w0, d.w0 + d.Wr) is written and counted.
 __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_sets, MsmDims d,
                                                             T* __restrict__ digits, uint32_t* __restrict__ colsum) {
   extern __shared__ uint32_t lds_hist[];  // [Wr][nbc]
@@ -359,8 +492,11 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
   const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
   const uint32_t w0 = blockIdx.y * d.Wr;
   const uint32_t nh = d.Wr * d.nbc;
-  for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) lds_hist[b] = 0;
+  [[maybe_unused]] const uint32_t pwg = blockIdx.y * gridDim.x + blockIdx.x;
+  PROBE(0, pwg, 0);
+  for (uint32_t b = threadIdx.x; b < nh + d.Wr; b += RC_THREADS) lds_hist[b] = 0;  // + the window totals
   __syncthreads();
+  PROBE(0, pwg, 1);
   // (loading all of a lane's scalars before recoding any measured slower: 43 vs 37 us per
   // two-MSM 2^20 launch)
   for (uint32_t i = lo + threadIdx.x; i < hi; i += RC_THREADS) {
@@ -379,99 +515,143 @@ __global__ void __launch_bounds__(RC_THREADS) k_recode_hist(BatchPtrs scalar_set
           return;
         }
         code = mag | (digit < 0 ? DigitCode<T>::SIGN : 0u);
-        atomicAdd(&lds_hist[w * d.nbc + (mag >> d.fb)], 1u);
+        atomicAdd(&lds_hist[w * d.nbc + (mag >> win_fb(d, wa))], 1u);
       }
       digits[(size_t)(w0 + w) * d.n + i] = (T)code;
     });
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nh; b += RC_THREADS) {
-    const uint32_t v = lds_hist[b];
-    if (v) atomicAdd(&colsum[w0 * d.nbc + b], v);
-  }
+  PROBE(0, pwg, 2);
+  flush_hist(lds_hist, d, w0, colsum);
+  PROBE(0, pwg, 7);
 }
 
-// k_fine_sort geometry (also decides which bins k_bin_scan lists for k_big_place)
+// The same with the geometry fixed at compile time (FixedGeo above) and 16-bit codes.  FULL: the
+// launch covers every window (no range, no half windows), so nothing per window is uniform but
+// the two fine-bit counts; else each window checks the range.  Row and histogram addresses advance
+// by a stride per window kept in the range.
+// (__launch_bounds__ with 8 waves per SIMD: two workgroups per CU need <= 80 SGPRs, which the
+// unrolled windows' constants otherwise exceed -- one workgroup per CU took 37 against 31 us.)
+template <uint32_t Q, uint32_t NHI, bool FULL>
+__global__ void __launch_bounds__(RC_THREADS, 8) k_recode_fixed(BatchPtrs scalar_sets, MsmDims d,
+                                                             uint16_t* __restrict__ digits,
+                                                             uint32_t* __restrict__ colsum) {
+  using G = FixedGeo<Q, NHI>;
+  using DC = DigitCode<uint16_t>;
+  static_assert(G::off(G::WMAIN) == MAIN_BITS, "main windows cover bits [0, 254)");
+  constexpr typename G::Words C = G::bias();
+  extern __shared__ uint32_t lds_hist[];  // [Wr][nbc]
+  const uint32_t* __restrict__ scalars = scalar_sets.p[blockIdx.y];
+  const uint32_t lo = blockIdx.x * RC_SPAN, hi = min(d.n, lo + RC_SPAN);
+  const uint32_t w0 = blockIdx.y * d.Wr;
+  const uint32_t nh = d.Wr * d.nbc;
+  [[maybe_unused]] const uint32_t pwg = blockIdx.y * gridDim.x + blockIdx.x;
+  PROBE(0, pwg, 0);
+  for (uint32_t b = threadIdx.x; b < nh + d.Wr; b += RC_THREADS) lds_hist[b] = 0;  // + the window totals
+  // fine bits of the wide (Q + 1) windows, the narrow (Q) ones and the overflow window (win_fb)
+  const uint32_t fb_w = d.fb - (d.c - (NHI ? Q + 1 : Q));
+  const uint32_t fb_n = d.fb > d.c - Q ? d.fb - (d.c - Q) : 0u;
+  const uint32_t fb_o = d.fb > d.c - OVF_BITS ? d.fb - (d.c - OVF_BITS) : 0u;
+  const uint32_t wlo = d.w0, whi = d.w0 + d.Wr;
+  __syncthreads();
+  PROBE(0, pwg, 1);
+  // Each lane recodes two adjacent scalars: their loads are one 64-B run, and a window's two
+  // codes go out as one 4-B store (when n is even, so that every row stays 4-B aligned).
+  const bool pair_store = (d.n & 1u) == 0;
+  for (uint32_t i = lo + 2 * threadIdx.x; i < hi; i += 2 * RC_THREADS) {
+    const bool two = i + 1 < hi;
+    uint32_t t0[8], t1[8], cy0 = 0, cy1 = 0;
+    {
+      uint32_t s0[8], s1[8];
+      load_scalar(scalars, i, s0);
+      if (two)
+        load_scalar(scalars, i + 1, s1);
+      else
+#pragma unroll
+        for (int k = 0; k < 8; k++) s1[k] = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t x0 = (uint64_t)s0[k] + C.v[k] + cy0;
+        const uint64_t x1 = (uint64_t)s1[k] + C.v[k] + cy1;
+        t0[k] = (uint32_t)x0;
+        t1[k] = (uint32_t)x1;
+        cy0 = (uint32_t)(x0 >> 32);
+        cy1 = (uint32_t)(x1 >> 32);
+      }
+    }
+    uint16_t* row = digits + (size_t)w0 * d.n + i;
+    uint32_t* h = lds_hist;
+#pragma unroll
+    for (uint32_t wa = 0; wa <= G::WMAIN; wa++) {
+      if (!FULL && (wa < wlo || wa >= whi)) continue;
+      int32_t dg[2];
+      uint32_t fbits, hb;
+      if (wa < G::WMAIN) {
+        const uint32_t o = G::off(wa), b = G::bits(wa), k = o / 32, sh = o % 32;
+        const uint32_t x0 = (sh + b <= 32 ? t0[k] >> sh : __builtin_amdgcn_alignbit(t0[k + 1], t0[k], sh)) & ((1u << b) - 1u);
+        const uint32_t x1 = (sh + b <= 32 ? t1[k] >> sh : __builtin_amdgcn_alignbit(t1[k + 1], t1[k], sh)) & ((1u << b) - 1u);
+        dg[0] = (int32_t)x0 - (int32_t)((1u << (b - 1)) - 1u);
+        dg[1] = (int32_t)x1 - (int32_t)((1u << (b - 1)) - 1u);
+        fbits = b == Q + 1 ? fb_w : fb_n;
+        hb = 1u << (b - 2);
+      } else {
+        dg[0] = (int32_t)((t0[7] >> 30) | (cy0 << 2));
+        dg[1] = (int32_t)((t1[7] >> 30) | (cy1 << 2));
+        fbits = fb_o;
+        hb = 1u << (OVF_BITS - 2);
+      }
+      uint32_t code[2];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int32_t digit = dg[q];
+        const uint32_t mag = (uint32_t)(digit < 0 ? -digit : digit) - 1u;
+        bool live = digit != 0 && (q == 0 || two);
+        if (!FULL) {
+          // half windows at the range's ends: a bucket outside the kept half is another share's
+          if (wa == wlo && d.half_lo) live = live && mag >= hb;
+          if (wa + 1 == whi && d.half_hi) live = live && mag < hb;
+        }
+        // every lane adds (0 for a zero digit): no divergent branch around the LDS atomic
+        atomicAdd(&h[live ? mag >> fbits : 0u], live ? 1u : 0u);
+        code[q] = live ? mag | (digit < 0 ? DC::SIGN : 0u) : DC::ZERO;
+      }
+      if (pair_store && two) {
+        *reinterpret_cast<uint32_t*>(row) = code[0] | code[1] << 16;
+      } else {
+        row[0] = (uint16_t)code[0];
+        if (two) row[1] = (uint16_t)code[1];
+      }
+      row += d.n;
+      h += d.nbc;
+    }
+  }
+  __syncthreads();
+  PROBE(0, pwg, 2);
+  flush_hist(lds_hist, d, w0, colsum);
+  PROBE(0, pwg, 7);
+}
+
+// k_fine_sort geometry
 #ifndef MSM_FS_THREADS
 #define MSM_FS_THREADS 512
 #endif
-constexpr uint32_t FS_THREADS = MSM_FS_THREADS;
-constexpr uint32_t FS_R = 6144 / FS_THREADS;
-constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // 6144 entries staged in LDS (512 threads: -12% vs 256, measured)
-constexpr uint32_t FS_MAXF = 2048;
-constexpr uint32_t FS_BIG = 65536;  // bins above this are placed tile-parallel by k_big_place
-
-// Exclusive scan of the bin totals colsum[0..nbins) into bin_base[0..nbins] (bin_base[nbins] =
-// total entries), with a copy in bin_cur (k_part_scatter's slice cursors); colsum is left zeroed
-// for the next MSM's atomics.  One workgroup, tiles of BS_TILE bins: a tile is staged in LDS with
-// coalesced loads, each thread scans a contiguous run of it, and the runs' sums are scanned per
-// wave (DPP) and across the 16 waves.  Also lists the tiles (FS_CAP entries) of bins too big for
-// k_fine_sort's LDS staging: big_tiles = [count, (bin, tile offset)...], consumed by k_big_place.
-constexpr uint32_t BS_THREADS = 1024;
-#ifndef MSM_BS_TILE
-#define MSM_BS_TILE 4096
+// Bins staged in LDS: up to FS_CAP entries.  A bin averages ~4K entries, but the top window of
+// scalars reduced mod r (< 0.58 * 2^253, as any prover's are) fills only 58% of its buckets, so
+// its bins hold ~7K: 8,192 keeps them on the staged path (at 6,144 they took the unstaged one and
+// were the kernel's stragglers, ~25 us each).
+#ifndef MSM_FS_CAP
+#define MSM_FS_CAP 8192
 #endif
-// 16 KiB of LDS per tile (64 KiB measured the same); a two-MSM 2^20 launch has 8,704 bins
-constexpr uint32_t BS_TILE = MSM_BS_TILE;
-extern "C" __global__ void __launch_bounds__(BS_THREADS) k_bin_scan(uint32_t* __restrict__ colsum,
-                                                                    uint32_t* __restrict__ bin_base,
-                                                                    uint32_t* __restrict__ bin_cur, uint32_t nbins,
-                                                                    uint32_t* __restrict__ big_tiles) {
-  __shared__ uint32_t sv[BS_TILE];
-  __shared__ uint32_t wtot[BS_THREADS / 64];
-  __shared__ uint32_t ntile, carry;
-  if (threadIdx.x == 0) ntile = carry = 0;
-  const uint32_t wave = threadIdx.x >> 6;
-  for (uint32_t t0 = 0; t0 < nbins; t0 += BS_TILE) {
-    const uint32_t nt = min(BS_TILE, nbins - t0);
-    for (uint32_t b = threadIdx.x; b < nt; b += BS_THREADS) {
-      sv[b] = colsum[t0 + b];
-      colsum[t0 + b] = 0;
-    }
-    __syncthreads();
-    const uint32_t per = (nt + BS_THREADS - 1) / BS_THREADS;
-    const uint32_t lo = min(nt, threadIdx.x * per), hi = min(nt, lo + per);
-    uint32_t sum = 0;
-    for (uint32_t k = lo; k < hi; k++) sum += sv[k];
-    uint32_t wsum;
-    const uint32_t wpre = wave_excl_scan(sum, wsum);
-    if ((threadIdx.x & 63) == 0) wtot[wave] = wsum;
-    __syncthreads();
-    uint32_t run = carry + wpre;
-    for (uint32_t v = 0; v < wave; v++) run += wtot[v];
-    for (uint32_t k = lo; k < hi; k++) {
-      const uint32_t m = sv[k];
-      sv[k] = run;
-      run += m;
-      if (m > FS_BIG) {
-        const uint32_t ntl = (m + FS_CAP - 1) / FS_CAP;
-        const uint32_t at = atomicAdd(&ntile, ntl);
-        for (uint32_t t = 0; t < ntl; t++) {
-          big_tiles[1 + 2 * (at + t)] = t0 + k;
-          big_tiles[2 + 2 * (at + t)] = t * FS_CAP;
-        }
-      }
-    }
-    __syncthreads();  // every thread has read carry
-    if (threadIdx.x == BS_THREADS - 1) carry = run;
-    for (uint32_t b = threadIdx.x; b < nt; b += BS_THREADS) {
-      const uint32_t v = sv[b];
-      bin_base[t0 + b] = v;
-      bin_cur[t0 + b] = v;
-    }
-    __syncthreads();  // the tile's LDS is reused, carry published
-  }
-  if (threadIdx.x == 0) {
-    bin_base[nbins] = carry;
-    big_tiles[0] = ntile;
-  }
-}
+constexpr uint32_t FS_THREADS = MSM_FS_THREADS;
+constexpr uint32_t FS_R = MSM_FS_CAP / FS_THREADS;
+constexpr uint32_t FS_CAP = FS_THREADS * FS_R;  // (512 threads: -12% vs 256 at 6,144, measured)
+constexpr uint32_t FS_MAXF = 2048;
 
 // Pass 2: each (window, chunk) workgroup moves its digits into its own contiguous slice of every
 // coarse bin.  The chunk is counting-sorted by bin inside LDS -- the LDS atomic that counts an
 // entry also returns its rank inside its bin, so every entry is placed without a second atomic
-// -- and each bin's slice is reserved with one global atomic on the bin's cursor (bin_cur, from
-// k_bin_scan; the slices' order inside a bin is immaterial: the bucket sums commute).  The
+// -- and each bin's slice is reserved with one global atomic on the bin's cursor (bin_cur, counted
+// from zero; the slices' order inside a bin is immaterial: the bucket sums commute).  The
 // staged chunk is then streamed out so that consecutive lanes write consecutive addresses of a
 // slice (>= 64 entries per slice by construction of ch).  (Writing each entry straight from
 // registers to its slice, with no LDS staging, measured 59 -> 153 us per two-MSM 2^20 launch; the
@@ -500,76 +680,133 @@ static_assert(PT_THREADS * PS_R == (1u << PS_POS) && PS_POS <= 16, "PartStage<ui
 
 template <typename T>
 __global__ void __launch_bounds__(PT_THREADS) k_part_scatter(const T* __restrict__ digits, MsmDims d,
+                                                             uint32_t* __restrict__ colsum,
                                                              uint32_t* __restrict__ bin_cur,
+                                                             uint32_t* __restrict__ bin_base,
                                                              uint32_t* __restrict__ part_entry,
                                                              uint16_t* __restrict__ part_fine) {
   using S = PartStage<T>;
   __shared__ typename S::V st[PT_THREADS * PS_R];
   __shared__ uint32_t m_live;
-  extern __shared__ uint32_t dyn[];  // [nbc] count -> local start, [nbc] global slice start
-  uint32_t* lcnt = dyn;
-  uint32_t* gstart = dyn + d.nbc;
+  __shared__ uint32_t wpart[PT_THREADS / 64];
+  // [nbc] count -> local start, [nbc] global slice start - local start, [nbc] bin start in window
+  extern __shared__ uint4 dyn4[];
+  uint32_t* lcnt = reinterpret_cast<uint32_t*>(dyn4);
+  uint32_t* gdel = lcnt + d.nbc;
+  uint32_t* bscan = gdel + d.nbc;
   const uint32_t w = blockIdx.y, ck = blockIdx.x;
+  const uint32_t fbw = batch_win_fb(d, w);
   const uint32_t pbase = d.shared ? 0u : (w / d.Wr) * d.n;  // first point record of this window's MSM
   const T* dw = digits + (size_t)w * d.n;
   const uint32_t lo = ck * d.ch, hi = min(d.n, lo + d.ch);
-  uint32_t code[PS_R], rank[PS_R];
+  [[maybe_unused]] const uint32_t pwg = blockIdx.y * gridDim.x + blockIdx.x;
+  PROBE(1, pwg, 0);
+  // 16-bit codes carry their rank in the bin in their upper half (one register per digit: the
+  // workgroup stays within 64 VGPRs, two per CU); 32-bit codes keep it apart
+  constexpr bool PACK = sizeof(T) == 2;
+  uint32_t code[PS_R], rank[PACK ? 1 : PS_R];
 #pragma unroll
   for (uint32_t r = 0; r < PS_R; r++) {
     const uint32_t i = lo + r * PT_THREADS + threadIdx.x;
     code[r] = i < hi ? (uint32_t)dw[i] : DigitCode<T>::ZERO;
   }
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) lcnt[b] = 0;
+  // Beside the digit loads: the window's bin totals (scanned below into the bins' starts inside
+  // the window) and the sum of the lower windows' totals (the window's first slot) -- what a
+  // separate one-workgroup scan kernel computed before (k_bin_scan, ~10 us per launch).
+  // nbc <= 256 <= PT_THREADS (make_plan): one bin per thread.
+  const bool bin_lane = threadIdx.x < d.nbc;
+  const uint32_t tot_b = bin_lane ? colsum[w * d.nbc + threadIdx.x] : 0u;
+  const uint32_t* wtot = colsum + d.nbins;
+  uint32_t lower = 0;
+  for (uint32_t v = threadIdx.x; v < w; v += PT_THREADS) lower += wtot[v];
+  lower = wave_incl_scan(lower);
+  if ((threadIdx.x & 63) == 63) wpart[threadIdx.x >> 6] = lower;
+  if (bin_lane) {
+    lcnt[threadIdx.x] = 0;
+    bscan[threadIdx.x] = tot_b;
+  }
+  PROBE_WAIT_VM();
+  PROBE(1, pwg, 1);
   __syncthreads();
 #pragma unroll
-  for (uint32_t r = 0; r < PS_R; r++)
-    if (code[r] != DigitCode<T>::ZERO) rank[r] = atomicAdd(&lcnt[(code[r] & DigitCode<T>::MAG) >> d.fb], 1u);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < d.nbc; b += PT_THREADS) {
-    const uint32_t c = lcnt[b];
-    gstart[b] = c ? atomicAdd(&bin_cur[w * d.nbc + b], c) : 0u;
-    if (b == d.nbc - 1) m_live = c;
+  for (uint32_t r = 0; r < PS_R; r++) {
+    if (code[r] != DigitCode<T>::ZERO) {
+      const uint32_t rk = atomicAdd(&lcnt[(code[r] & DigitCode<T>::MAG) >> fbw], 1u);
+      if constexpr (PACK)
+        code[r] |= rk << 16;
+      else
+        rank[r] = rk;
+    }
   }
+  lds_excl_scan_wave0(bscan, d.nbc);
   __syncthreads();
+  PROBE(1, pwg, 2);
+  // each bin's slice is reserved with one global atomic on the bin's cursor (zero-based; its
+  // latency overlaps the local scan)
+  const uint32_t cb = bin_lane ? lcnt[threadIdx.x] : 0u;
+  const uint32_t g = cb ? atomicAdd(&bin_cur[w * d.nbc + threadIdx.x], cb) : 0u;
+  if (threadIdx.x == d.nbc - 1) m_live = cb;
+  uint32_t wbase = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PT_THREADS / 64; k++) wbase += wpart[k];
+  __syncthreads();
+  PROBE(1, pwg, 3);
   lds_excl_scan_wave0(lcnt, d.nbc);
   __syncthreads();
+  PROBE(1, pwg, 4);
+  if (bin_lane) {
+    const uint32_t start = wbase + bscan[threadIdx.x];  // the bin's first slot in the sorted order
+    gdel[threadIdx.x] = start + g - lcnt[threadIdx.x];  // entry j of bin b goes to j + gdel[b]
+    if (ck == 0) {
+      bin_base[w * d.nbc + threadIdx.x] = start;
+      if (w + 1 == d.W && threadIdx.x == d.nbc - 1) bin_base[d.nbins] = start + tot_b;
+    }
+  }
 #pragma unroll
-  for (uint32_t r = 0; r < PS_R; r++)
-    if (code[r] != DigitCode<T>::ZERO)
-      st[lcnt[(code[r] & DigitCode<T>::MAG) >> d.fb] + rank[r]] = S::pack(code[r], r * PT_THREADS + threadIdx.x);
+  for (uint32_t r = 0; r < PS_R; r++) {
+    const uint32_t cd = PACK ? code[r] & 0xffffu : code[r];
+    if (cd != DigitCode<T>::ZERO)
+      st[lcnt[(cd & DigitCode<T>::MAG) >> fbw] + (PACK ? code[r] >> 16 : rank[PACK ? 0 : r])] =
+          S::pack(cd, r * PT_THREADS + threadIdx.x);
+  }
   __syncthreads();
+  PROBE(1, pwg, 5);
   const uint32_t m = lcnt[d.nbc - 1] + m_live;  // live digits of the chunk
-  const uint32_t fmask = (1u << d.fb) - 1u;
+  const uint32_t fmask = (1u << fbw) - 1u;
   for (uint32_t j = threadIdx.x; j < m; j += PT_THREADS) {
     const typename S::V v = st[j];
     const uint32_t cd = S::code(v);
     const uint32_t b = cd & DigitCode<T>::MAG;
-    const uint32_t bin = b >> d.fb, fine = b & fmask;
+    const uint32_t fine = b & fmask;
     const uint32_t ent = ((pbase + lo + S::pos(v)) << 1) | (cd >> DigitCode<T>::SHIFT);
-    const uint32_t dst = gstart[bin] + (j - lcnt[bin]);
+    const uint32_t dst = j + gdel[b >> fbw];
+    // packed: the fine key in the low d.fb bits (a narrower window's fbw <= d.fb of them used)
     part_entry[dst] = d.packed ? (ent << d.fb) | fine : ent;
     if (!d.packed) part_fine[dst] = (uint16_t)fine;
   }
+  PROBE(1, pwg, 6);
+  PROBE(1, pwg, 7);
 }
 
 // Pass 3: one workgroup per coarse bin, counting sort by fine bucket (<= FS_MAXF per bin).  A bin
 // of at most FS_CAP entries is sorted inside LDS and streamed out coalesced.  Besides the sorted
 // entry list it writes the bucket boundaries the accumulation walks: bucket_start[key] (global
 // position of bucket `key`'s first entry; bucket_start[W*B] = bucket_start[W*B+1] = total) and
-// run_key[r] = the bucket holding position r*K (the first entry of accumulation run r).
+// run_key[r] = the bucket holding position r*K (the first entry of accumulation run r).  A window
+// narrower than the widest has fewer buckets than B (win_fb): the bins' workgroups also set its
+// keys past them, each a share, to the window's end.
 //
-// A bin of up to FS_BIG entries (e.g. the dense top window) is placed here tile by tile with
-// direct scatters.  A bigger one (skewed scalars) is only counted here -- boundaries, run keys
-// and one placement cursor per bucket -- and its entries are placed by k_big_place, whose
-// workgroups share the bin tile by tile.  Counting collapses runs of equal keys per lane before
-// touching LDS, so a bin that is one giant bucket costs one atomic per lane, not per entry.
+// A bigger bin (skewed scalars: one giant bucket, or few distinct digits) is sorted by its own
+// workgroup in register tiles: a counting pass that collapses runs of equal keys per lane before
+// touching LDS (a bin that is one giant bucket costs one atomic per lane, not per entry), then a
+// placement pass in which the lanes of a wave holding the same key find each other by ballots over
+// the key's bits and their leader reserves all their slots with one atomic -- so equal keys never
+// serialise on one LDS address, and they are written coalesced.  (This replaced k_big_place, a
+// tile-parallel kernel of its own that cost a launch, ~5 us, on every MSM for the skewed inputs'
+// sake.)
 
 // One coarse-binned entry: its fine key (bucket within the bin) and the sorted-list entry
 // (idx << 1 | sign), from the packed word or the two arrays (MsmDims::packed).
-__device__ __forceinline__ uint32_t part_fine_at(const uint32_t* __restrict__ pe, const uint16_t* __restrict__ pf,
-                                                 const MsmDims& d, uint32_t i) {
-  return d.packed ? pe[i] & ((1u << d.fb) - 1u) : (uint32_t)pf[i];
-}
 __device__ __forceinline__ void part_load(const uint32_t* __restrict__ pe, const uint16_t* __restrict__ pf,
                                           const MsmDims& d, uint32_t i, uint32_t& fine, uint32_t& entry) {
   const uint32_t v = pe[i];
@@ -592,34 +829,73 @@ __device__ __forceinline__ void count_runs(uint32_t* cnt, uint32_t& last, uint32
   }
 }
 
-extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint32_t* __restrict__ part_entry,
+// Lanes of the wave whose `key` (fbits bits) equals this lane's, among the lanes in `live`.
+__device__ __forceinline__ uint64_t key_peers(uint32_t key, uint32_t fbits, uint64_t live) {
+  uint64_t peers = live;
+  for (uint32_t b = 0; b < fbits; b++) {
+    const uint64_t set = __ballot((key >> b) & 1u);
+    peers &= ((key >> b) & 1u) ? set : ~set;
+  }
+  return peers;
+}
+
+// MSM_FS_MINW: minimum waves per SIMD asked of the compiler.  8 = four workgroups per CU (<= 64
+// VGPRs, a few spilled in the unstaged path): 57 against 63 us per two-MSM 2^20 launch at 76 VGPRs
+// (three workgroups per CU).
+#ifndef MSM_FS_MINW
+#define MSM_FS_MINW 8
+#endif
+#if MSM_FS_MINW > 0
+#define FS_BOUNDS __launch_bounds__(FS_THREADS, MSM_FS_MINW)
+#else
+#define FS_BOUNDS __launch_bounds__(FS_THREADS)
+#endif
+extern "C" __global__ void FS_BOUNDS k_fine_sort(const uint32_t* __restrict__ part_entry,
                                                                      const uint16_t* __restrict__ part_fine,
                                                                      const uint32_t* __restrict__ bin_base, MsmDims d,
                                                                      uint32_t K, uint32_t* __restrict__ sorted_entry,
                                                                      uint32_t* __restrict__ bucket_start,
                                                                      uint32_t* __restrict__ run_key,
-                                                                     uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t cnt[FS_MAXF];
+                                                                     uint32_t* __restrict__ colsum,
+                                                                     uint32_t* __restrict__ bin_cur) {
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[FS_MAXF];
   __shared__ uint32_t st_entry[FS_CAP];
   const uint32_t bin = blockIdx.x;
-  const uint32_t nf = 1u << d.fb;
+  PROBE(2, bin, 0);
+  const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
+  const uint32_t fbw = batch_win_fb(d, w);
+  const uint32_t nf = 1u << fbw;
   const uint32_t base = bin_base[bin];
   const uint32_t m = bin_base[bin + 1] - base;
-  const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
-  const uint32_t key0 = w * d.B + (cb << d.fb);
+  const uint32_t key0 = w * d.B + (cb << fbw);
   for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
+  if (threadIdx.x == 0) {
+    // the bin's total, cursor and window total are consumed (k_part_scatter): zero for the next MSM
+    colsum[bin] = 0;
+    bin_cur[bin] = 0;
+    if (cb == 0) colsum[d.nbins + w] = 0;
+  }
   if (bin + 1 == gridDim.x && threadIdx.x == 0) {
     bucket_start[d.W * d.B] = base + m;
     bucket_start[d.W * d.B + 1] = base + m;
   }
+  {
+    // a narrower window's keys past its buckets: empty, all at the window's end
+    const uint32_t k1 = d.nbc << fbw;
+    if (k1 < d.B) {
+      const uint32_t span = (d.B - k1) / d.nbc, wend = bin_base[(w + 1) * d.nbc];
+      for (uint32_t f = threadIdx.x; f < span; f += FS_THREADS) bucket_start[w * d.B + k1 + cb * span + f] = wend;
+    }
+  }
   __syncthreads();
+  PROBE(2, bin, 1);
   const bool staged = m <= FS_CAP;
+  const uint32_t fmask = (1u << d.fb) - 1u;  // the packed word's fine field (fbw <= d.fb bits used)
   // fk: fine key (< 2^11) of a staged entry, later | its rank in its bucket << 16 (< FS_CAP)
   uint32_t fk[FS_R], en[FS_R];
   if (staged) {
     // every load issued before any is used; the packed/unpacked choice is uniform
     if (d.packed) {
-      const uint32_t fmask = (1u << d.fb) - 1u;
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
         const uint32_t e = r * FS_THREADS + threadIdx.x;
@@ -631,6 +907,8 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
         fk[r] = e < m ? en[r] & fmask : 0xffffu;
         en[r] >>= d.fb;
       }
+      PROBE_WAIT_VM();
+      PROBE(2, bin, 2);
     } else {
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
@@ -650,7 +928,9 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
         const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
-        fk[r] = e < m ? part_fine_at(part_entry, part_fine, d, base + e) : 0xffffu;
+        uint32_t en_unused;
+        fk[r] = 0xffffu;
+        if (e < m) part_load(part_entry, part_fine, d, base + e, fk[r], en_unused);
       }
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++)
@@ -659,10 +939,12 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
     if (run) atomicAdd(&cnt[last], run);
   }
   __syncthreads();
+  PROBE(2, bin, 3);
   // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them (a bucket
   // ends where the next one starts)
   lds_excl_scan_wave0(cnt, nf);
   __syncthreads();
+  PROBE(2, bin, 4);
 #pragma unroll
   for (uint32_t q = 0; q < FS_MAXF / FS_THREADS; q++) {
     const uint32_t f = q * FS_THREADS + threadIdx.x;
@@ -670,79 +952,46 @@ extern "C" __global__ void __launch_bounds__(FS_THREADS) k_fine_sort(const uint3
       const uint32_t gs = base + cnt[f];
       const uint32_t ge = base + (f + 1 < nf ? cnt[f + 1] : m);
       bucket_start[key0 + f] = gs;
-      if (m > FS_BIG) cursor[key0 + f] = gs;
       for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
     }
   }
-  if (m > FS_BIG) return;  // k_big_place moves the entries
   __syncthreads();
+  PROBE(2, bin, 5);
   if (!staged) {
+    // placement: a wave's lanes with equal keys take consecutive slots of their bucket, reserved
+    // by the lowest of them with one LDS atomic
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t t0 = 0; t0 < m; t0 += FS_CAP) {
 #pragma unroll
       for (uint32_t r = 0; r < FS_R; r++) {
         const uint32_t e = t0 + r * FS_THREADS + threadIdx.x;
-        if (d.packed) {
-          const uint32_t v = e < m ? part_entry[base + e] : 0u;
-          fk[r] = e < m ? v & ((1u << d.fb) - 1u) : 0xffffu;
-          en[r] = v >> d.fb;
-        } else {
-          fk[r] = e < m ? part_fine[base + e] : 0xffffu;
-          en[r] = e < m ? part_entry[base + e] : 0u;
-        }
+        fk[r] = 0u;
+        en[r] = 0u;
+        if (e < m) part_load(part_entry, part_fine, d, base + e, fk[r], en[r]);
       }
 #pragma unroll
-      for (uint32_t r = 0; r < FS_R; r++)
-        if (fk[r] != 0xffffu) sorted_entry[base + atomicAdd(&cnt[fk[r]], 1u)] = en[r];
+      for (uint32_t r = 0; r < FS_R; r++) {
+        const bool live = t0 + r * FS_THREADS + threadIdx.x < m;
+        const uint64_t peers = key_peers(fk[r], fbw, __ballot(live));
+        const uint32_t leader = (uint32_t)__builtin_ctzll(peers | (1ull << 63));
+        uint32_t slot = 0;
+        if (live && lane == leader) slot = atomicAdd(&cnt[fk[r]], (uint32_t)__popcll(peers));
+        slot = (uint32_t)__shfl((int)slot, (int)leader, 64);
+        if (live) sorted_entry[base + slot + (uint32_t)__popcll(peers & below)] = en[r];
+      }
     }
+    PROBE(2, bin, 6);
+    PROBE(2, bin, 7);
     return;
   }
 #pragma unroll
   for (uint32_t r = 0; r < FS_R; r++)
     if (fk[r] != 0xffffu) st_entry[cnt[fk[r] & 0xffffu] + (fk[r] >> 16)] = en[r];
   __syncthreads();
+  PROBE(2, bin, 6);
   for (uint32_t j = threadIdx.x; j < m; j += FS_THREADS) sorted_entry[base + j] = st_entry[j];
-}
-
-// Placement for bins larger than FS_CAP: workgroups stride over the tiles (FS_CAP entries) of
-// every big bin.  Per tile: LDS histogram of fine keys (runs of equal keys collapsed), one
-// global reservation per (tile, bucket) on the bucket's cursor, then each entry takes the next
-// slot of its bucket's reserved range.  The order inside a bucket is irrelevant to the sum.
-constexpr uint32_t BP_GRID = 512;
-extern "C" __global__ void __launch_bounds__(FS_THREADS) k_big_place(const uint32_t* __restrict__ part_entry,
-                                                                     const uint16_t* __restrict__ part_fine,
-                                                                     const uint32_t* __restrict__ bin_base, MsmDims d,
-                                                                     const uint32_t* __restrict__ big_tiles,
-                                                                     uint32_t* __restrict__ cursor,
-                                                                     uint32_t* __restrict__ sorted_entry) {
-  const uint32_t ntiles = big_tiles[0];
-  if (blockIdx.x >= ntiles) return;
-  __shared__ uint32_t cnt[FS_MAXF];
-  const uint32_t nf = 1u << d.fb;
-  for (uint32_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
-    const uint32_t bin = big_tiles[1 + 2 * ti], t0 = big_tiles[2 + 2 * ti];
-    const uint32_t base = bin_base[bin];
-    const uint32_t m = min(bin_base[bin + 1] - base - t0, FS_CAP);
-    const uint32_t w = bin / d.nbc, cb = bin % d.nbc;
-    const uint32_t key0 = w * d.B + (cb << d.fb);
-    for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) cnt[f] = 0;
-    __syncthreads();
-    uint32_t last = 0, run = 0;
-    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS)
-      count_runs(cnt, last, run, part_fine_at(part_entry, part_fine, d, base + t0 + e));
-    if (run) atomicAdd(&cnt[last], run);
-    __syncthreads();
-    for (uint32_t f = threadIdx.x; f < nf; f += FS_THREADS) {
-      const uint32_t c = cnt[f];
-      if (c) cnt[f] = atomicAdd(&cursor[key0 + f], c);
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < m; e += FS_THREADS) {
-      uint32_t f, en;
-      part_load(part_entry, part_fine, d, base + t0 + e, f, en);
-      sorted_entry[atomicAdd(&cnt[f], 1u)] = en;
-    }
-    __syncthreads();
-  }
+  PROBE(2, bin, 7);
 }
 
 // ---------------------------------------------------------------------------------------------

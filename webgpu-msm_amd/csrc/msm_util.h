@@ -3,6 +3,10 @@
 // point; src/reference/webgpu/utils.ts:81-100, scalars uniform mod p) with a deterministic
 // spec: P_i = (k0 + i step) G, scalars from xorshift64.
 #pragma once
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -55,8 +59,26 @@ static inline void gen_points_range(const Pt& g, uint64_t k0, uint64_t step, siz
   }
 }
 
+// Threads the host can run at once: the hardware threads, capped by a cgroup-v2 CPU quota
+// (/sys/fs/cgroup/cpu.max = "quota period"): a container reports the whole machine's threads
+// (256 on an MI355X node) while its quota may allow 16, and 256 threads on 16 CPUs thrash.
+static inline unsigned host_threads() {
+  static const unsigned t = [] {
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {0};
+      unsigned long long period = 0;
+      if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0)
+        hw = (unsigned)std::min<unsigned long long>(hw, std::max(1ull, strtoull(quota, nullptr, 10) / period));
+      fclose(f);
+    }
+    return hw;
+  }();
+  return t;
+}
+
 static inline void gen_points(const Pt& g, uint64_t k0, uint64_t step, size_t n, uint32_t* out) {
-  unsigned th = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  unsigned th = std::max(1u, std::min(64u, host_threads()));
   if (n < 4096) th = 1;
   std::vector<std::thread> ts;
   size_t per = (n + th - 1) / th;

@@ -27,6 +27,7 @@
 #include <node_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -444,7 +445,17 @@ napi_value StrError(napi_env env, napi_callback_info info) {
   return r;
 }
 
+// Explicit teardown when the last environment that loaded the addon is torn down (process exit
+// of the main thread, or the last worker): the library's streams, buffers and parked pool threads
+// are released and joined then, not left to the shared objects' finalizers.  (A call in flight
+// holds its device context, which msm_shutdown waits for.)
+std::atomic<int> g_envs{0};
+void CleanupEnv(void*) {
+  if (g_envs.fetch_sub(1) == 1) msm_shutdown();
+}
+
 napi_value ModuleInit(napi_env env, napi_value exports) {
+  if (napi_add_env_cleanup_hook(env, CleanupEnv, nullptr) == napi_ok) g_envs.fetch_add(1);
   napi_property_descriptor props[] = {
       {"computeMsmU32", nullptr, ComputeMsmU32, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"computeMsmBigInt", nullptr, ComputeMsmBigInt, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -12,6 +12,7 @@ raise MsmError.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 from typing import Iterable, Optional, Sequence, Tuple, Union
@@ -140,6 +141,7 @@ def load() -> ctypes.CDLL:
         "msm_test_tail_batch": ([sz, ctypes.c_uint32, vp, ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "msm_test_peer_state": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "msm_test_host_timing": ([ctypes.c_int, sz, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "msm_test_pools": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         if name.startswith("msm_test_") and not hasattr(L, name):
@@ -148,7 +150,16 @@ def load() -> ctypes.CDLL:
         f.argtypes = args
         f.restype = res
     _lib = L
+    # Explicit teardown at interpreter exit (registered after torch's import, so it runs before
+    # torch's own exit handlers): the library's streams, buffers and parked pool threads are released
+    # and joined while the HIP runtime is still whole, not left to the shared objects' finalizers.
+    atexit.register(_shutdown_at_exit)
     return L
+
+
+def _shutdown_at_exit() -> None:
+    if _lib is not None:
+        _lib.msm_shutdown()
 
 
 def _strerror(code: int) -> str:
