@@ -155,6 +155,9 @@ struct Workspace {
   Buf lead_val, lead_open, cross_key, lead_flag, skew_list, g_head, g_hkey, g_tkey, red_U, red_T;
   Buf wire_pts, wire_sc;  // device copies of host-resident inputs (msm_compute*, host entries)
   Buf red_G;               // k_red2_groups' points per (window, group of RG_CH chunks)
+#ifdef MSM_DUMMY_ALLOC
+  Buf dummy_tiles, dummy_cursor;  // tuning builds: the round-5 allocation layout
+#endif
   void release() {
     Buf* bufs[] = {&pts, &err, &digits, &colsum, &bin_base, &bin_cur, &part_entry, &part_fine,
                    &sorted_entry, &bucket_start, &run_key, &buckets, &lead_val, &lead_open, &cross_key,
@@ -575,6 +578,10 @@ int ensure_workspace(DevCtx* c, const Plan& pl, int si) {
   ENS(sorted_entry, pl.Mmax * 4 + 16);  // + a 16-B tail for k_accumulate's vector entry loads
   ENS(bucket_start, (nb + 2) * 4);
   ENS(run_key, pl.runs_max * 4);
+#ifdef MSM_DUMMY_ALLOC
+  ENS(dummy_tiles, (pl.Mmax / FS_CAP + d.nbins + 1) * 8 + 8);
+  ENS(dummy_cursor, nb * 4);
+#endif
   ENS(buckets, nb * PT_WORDS * 4);
   const size_t nwg = pl.runs_max / ACC_THREADS + 2;
   ENS(lead_val, nwg * PT_WORDS * 4);
@@ -754,6 +761,9 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
                        w.part_fine.as<uint16_t>(), w.bin_base.as<uint32_t>(), d, pl.K, w.sorted_entry.as<uint32_t>(),
                        w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), w.colsum.as<uint32_t>(),
                        w.bin_cur.as<uint32_t>());
+#ifdef MSM_GAP_KERNEL
+    hipLaunchKernelGGL(k_gap, dim3(MSM_GAP_KERNEL), dim3(64), 0, s, w.err.as<uint32_t>());
+#endif
     mark(PH_FINE);
   }
   if (fork) HIPCHECK(hipStreamWaitEvent(s, sl.ev_join, 0));

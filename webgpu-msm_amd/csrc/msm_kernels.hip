@@ -994,6 +994,13 @@ extern "C" __global__ void FS_BOUNDS k_fine_sort(const uint32_t* __restrict__ pa
   PROBE(2, bin, 7);
 }
 
+#ifdef MSM_GAP_KERNEL
+// tuning builds: a no-op launch between the sort and the accumulation
+extern "C" __global__ void k_gap(uint32_t* __restrict__ p) {
+  if (p == nullptr && threadIdx.x == 1234567) p[0] = 0;
+}
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // bucket accumulation
 // ---------------------------------------------------------------------------------------------

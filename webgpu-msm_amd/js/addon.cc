@@ -398,6 +398,78 @@ napi_value Split(napi_env env, napi_callback_info info) {
   return make_u32(env, out.data(), (size_t)nw * n);
 }
 
+// flattenU32(points, scalars, pointWords, scalarWords): U32ArrayPoint[] / Uint32Array[] into flat
+// wire buffers (x|y|t|z BE words per point, submission.ts:75-86), natively: per point one property
+// read per coordinate (keys made once) and one typed-array lookup, then a 32-B copy.  The A/B
+// against the JS loop (flattenU32 in submission.mjs) is tools/node_flatten_ab.mjs.
+napi_value FlattenU32(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  if (argc < 4) {
+    napi_throw_type_error(env, nullptr, "flattenU32(points, scalars, pointWords, scalarWords)");
+    return nullptr;
+  }
+  uint32_t np_ = 0, ns = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &np_));
+  NAPI_OK(napi_get_array_length(env, argv[1], &ns));
+  const uint32_t n = std::min(np_, ns);
+  const uint32_t *pwc = nullptr, *swc = nullptr;
+  size_t plen = 0, slen = 0;
+  if (!get_u32_array(env, argv[2], &pwc, &plen) || !get_u32_array(env, argv[3], &swc, &slen) ||
+      plen < (size_t)n * 32 || slen < (size_t)n * 8) {
+    napi_throw_type_error(env, nullptr, "pointWords / scalarWords must be Uint32Arrays of n x 32 / n x 8 words");
+    return nullptr;
+  }
+  uint32_t* pw = const_cast<uint32_t*>(pwc);  // the caller's output buffers
+  uint32_t* sw = const_cast<uint32_t*>(swc);
+  static const char* names[4] = {"x", "y", "t", "z"};
+  napi_value keys[4];
+  for (int k = 0; k < 4; k++) NAPI_OK(napi_create_string_utf8(env, names[k], 1, &keys[k]));
+  constexpr uint32_t BLOCK = 1024;
+  const char* bad = nullptr;
+  for (uint32_t i0 = 0; i0 < n && !bad; i0 += BLOCK) {
+    napi_handle_scope scope;
+    if (napi_open_handle_scope(env, &scope) != napi_ok) {
+      bad = "bad input element";
+      break;
+    }
+    const uint32_t i1 = std::min<uint32_t>(n, i0 + BLOCK);
+    for (uint32_t i = i0; i < i1 && !bad; i++) {
+      napi_value p, s;
+      const uint32_t* src;
+      size_t len;
+      if (napi_get_element(env, argv[0], i, &p) != napi_ok || napi_get_element(env, argv[1], i, &s) != napi_ok) {
+        bad = "bad input element";
+        break;
+      }
+      for (int k = 0; k < 4 && !bad; k++) {
+        napi_value c;
+        if (napi_get_property(env, p, keys[k], &c) != napi_ok || !get_u32_array(env, c, &src, &len) || len < 8)
+          bad = "point coordinates must be Uint32Arrays of 8 words";
+        else
+          memcpy(pw + (size_t)i * 32 + 8 * k, src, 32);
+      }
+      if (!bad) {
+        if (!get_u32_array(env, s, &src, &len) || len < 8)
+          bad = "scalars must be Uint32Arrays of 8 words";
+        else
+          memcpy(sw + (size_t)i * 8, src, 32);
+      }
+    }
+    napi_close_handle_scope(env, scope);
+  }
+  if (bad) {
+    bool pending = false;
+    napi_is_exception_pending(env, &pending);
+    if (!pending) napi_throw_type_error(env, nullptr, bad);
+    return nullptr;
+  }
+  napi_value r;
+  NAPI_OK(napi_create_uint32(env, n, &r));
+  return r;
+}
+
 napi_value BestWindowSize(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -461,6 +533,7 @@ napi_value ModuleInit(napi_env env, napi_value exports) {
       {"computeMsmBigInt", nullptr, ComputeMsmBigInt, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"pointAddAffine", nullptr, PointAddAffine, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"split", nullptr, Split, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"flattenU32", nullptr, FlattenU32, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"bestWindowSize", nullptr, BestWindowSize, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"init", nullptr, Init, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
