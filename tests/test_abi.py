@@ -52,7 +52,34 @@ def test_addon_exports():
         script = f"const a = require({addon!r}); console.log(Object.keys(a).sort().join(','))"
         keys = subprocess.run([node, "-e", script], capture_output=True, text=True, check=True).stdout.strip()
         assert keys.split(",") == sorted(["computeMsmU32", "computeMsmBigInt", "pointAddAffine", "split",
-                                          "bestWindowSize", "init", "deviceCount", "deviceOrdinals", "strerror"])
+                                          "bestWindowSize", "init", "deviceCount", "deviceOrdinals", "strerror",
+                                          "flattenU32"])
+
+
+def test_addon_native_flatten_matches_js():
+    # the native flatten (measured slower than the JS loop, tools/node_flatten_ab.mjs) writes the
+    # same wire words, and rejects coordinates that are not 8-word Uint32Arrays
+    node = shutil.which("node")
+    if not node:
+        pytest.skip("node not installed")
+    js = os.path.join(ROOT, "webgpu-msm_amd", "js", "submission.mjs")
+    addon = os.path.join(ROOT, "webgpu-msm_amd", "js", "msm_napi.node")
+    script = f"""
+import {{ createRequire }} from "module";
+import {{ flattenU32 }} from {js!r};
+const a = createRequire({addon!r})({addon!r});
+const mk = (k) => Uint32Array.from({{length: 8}}, (_, i) => (k * 8 + i) * 2654435761 >>> 0);
+const pts = [], sc = [];
+for (let i = 0; i < 37; i++) {{ pts.push({{x: mk(4 * i), y: mk(4 * i + 1), t: mk(4 * i + 2), z: mk(4 * i + 3)}}); sc.push(mk(999 + i)); }}
+const [pb, sb] = flattenU32(pts, sc);
+const pw = new Uint32Array(37 * 32), sw = new Uint32Array(37 * 8);
+const n = a.flattenU32(pts, sc, pw, sw);
+let bad = 0;
+try {{ a.flattenU32([{{x: [1], y: mk(0), t: mk(0), z: mk(0)}}], [mk(1)], pw, sw); }} catch (e) {{ bad = 1; }}
+console.log(JSON.stringify({{n, same: pb.every((v, i) => v === pw[i]) && sb.every((v, i) => v === sw[i]), bad}}));
+"""
+    r = subprocess.run([node, "--input-type=module", "-e", script], capture_output=True, text=True, check=True)
+    assert json.loads(r.stdout) == {"n": 37, "same": True, "bad": 1}
 
 
 def test_addon_bigint_marshalling_errors():
