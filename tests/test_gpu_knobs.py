@@ -58,6 +58,9 @@ print(json.dumps(out))
     {"MSM_HORNER_THREADS": "0", "MSM_FORK_PREP_PIPE": "1"},  # tails inline, preparation forked
     {"MSM_HOST_SORT_EARLY": "0", "MSM_HOST_PACK_THREADS": "1"},
     {"MSM_PIN_MAX_MB": "1"},                       # staging ring over its cap: every entry unpacked
+    {"MSM_RED1_PAIRS": "1"},                       # first reduction stage on lane pairs
+    {"MSM_RED_FOLD": "1"},                         # first stage and group trees in one launch
+    {"MSM_RECODE_FIXED": "0"},                     # the generic recode loop at every width
 ])
 def test_knob_paths_bit_exact(env):
     e = dict(os.environ)
@@ -66,3 +69,26 @@ def test_knob_paths_bit_exact(env):
                        timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1]) == [True, True, True], (env, r.stdout[-500:])
+
+
+TAIL_CHILD = r"""
+import json, sys
+sys.path[:0] = [{root!r}, {root!r} + "/webgpu-msm_amd", {root!r} + "/tests"]
+import msm_amd as M
+from _closed_form import closed_form
+n = 1 << 22
+pts = M.gen_points(n, k0=5, step=3)
+sc = M.gen_scalars(n, seed=2024)
+print(json.dumps(M.compute_msm_wire(pts, sc) == closed_form(5, 3, sc)))
+"""
+
+
+def test_tail_slices_longer_than_body_slices():
+    # MSM_HOST_TAIL_LOG = 18 at 2^22 points asks for tail slices of 2^18 while the body's 16 slices
+    # hold (2^22 - 2^19) / 16 = 229,376: the tail is dropped (every slice runs as an MSM of the
+    # body's length; a longer tail slice would lose points, ADVICE r5)
+    e = dict(os.environ, MSM_HOST_TAIL_LOG="18")
+    r = subprocess.run([sys.executable, "-c", TAIL_CHILD.format(root=ROOT)], env=e, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) is True

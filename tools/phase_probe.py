@@ -22,7 +22,7 @@ import numpy as np  # noqa: E402
 KERNELS = {0: ("k_recode_hist", {1: "zero", 2: "recode", 7: "flush"}),
            1: ("k_part_scatter", {1: "load", 2: "rank", 3: "reserve", 4: "scan", 5: "stage", 6: "store"}),
            2: ("k_fine_sort", {1: "head", 2: "load", 3: "rank", 4: "scan", 5: "bounds", 6: "stage", 7: "store"}),
-           3: ("k_extra", {})}
+           3: ("k_accumulate", {7: "all"})}
 WG, SLOTS = 16384, 10
 
 

@@ -549,6 +549,25 @@ int finish_plan(const MsmDims& d, const msm_opts* o, const DevShape& sh, Plan* p
   return MSM_OK;
 }
 
+// The first bucket-reduction stage and the second's group trees in one launch (k_bucket_reduce_1g,
+// MSM_RED_FOLD=1, where the tree form of the second stage applies; default k_bucket_reduce_1 then
+// k_red2_groups).  Measured slower: 287 against 157 + 31 us per two-MSM 2^20 launch -- a group's
+// tree then runs on two waves of 226-VGPR lanes (the first stage's occupancy) instead of eight
+// light ones.
+bool red_fold() {
+  static const bool on = getenv("MSM_RED_FOLD") && atoi(getenv("MSM_RED_FOLD")) != 0;
+  return on;
+}
+
+// The first bucket-reduction stage on lane pairs (k_bucket_reduce_1p, MSM_RED1_PAIRS=1; default one
+// lane per chunk, k_bucket_reduce_1).  Measured equal: 159-162 against 160 us per two-MSM 2^20
+// launch at three or four waves per SIMD, 154 at L = 8 but with the second stage then 51 against
+// 31 us -- the chains' adds are issue-bound, not latency-bound.
+bool red1_pairs() {
+  static const bool on = getenv("MSM_RED1_PAIRS") && atoi(getenv("MSM_RED1_PAIRS")) != 0;
+  return on;
+}
+
 // The second bucket-reduction stage as k_red2_groups + k_red2_terms (default; MSM_RED2_TREE=0:
 // k_bucket_reduce_2), for windows of at most RG_MAXG groups of RG_CH chunks (k_bucket_reduce_2
 // past that).  Single stream, 2^20, two MSMs per launch: 50 against 58 us.
@@ -789,24 +808,42 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   }
   if (parts & PART_POST) {
     mark(PH_FIXUP);
-    auto red1 = pl.L == 4    ? k_bucket_reduce_1<4>
-                : pl.L == 9  ? k_bucket_reduce_1<9>
-                : pl.L == 10 ? k_bucket_reduce_1<10>
-                : pl.L == 12 ? k_bucket_reduce_1<12>
-                : pl.L == 16 ? k_bucket_reduce_1<16>
-                : pl.L == 17 ? k_bucket_reduce_1<17>
-                : pl.L == 20 ? k_bucket_reduce_1<20>
-                             : k_bucket_reduce_1<8>;
-    hipLaunchKernelGGL(red1, dim3(grid_for((size_t)d.W * pl.nchunks, RED1_THREADS)), dim3(RED1_THREADS), 0, s,
+    const bool fold = red_fold() && red2_tree(pl);
+    if (fold) {
+      const uint32_t G = red2_groups(pl);
+      auto red1g = pl.L == 4    ? k_bucket_reduce_1g<4>
+                   : pl.L == 9  ? k_bucket_reduce_1g<9>
+                   : pl.L == 10 ? k_bucket_reduce_1g<10>
+                   : pl.L == 12 ? k_bucket_reduce_1g<12>
+                   : pl.L == 16 ? k_bucket_reduce_1g<16>
+                   : pl.L == 17 ? k_bucket_reduce_1g<17>
+                   : pl.L == 20 ? k_bucket_reduce_1g<20>
+                                : k_bucket_reduce_1g<8>;
+      hipLaunchKernelGGL(red1g, dim3(d.W * G), dim3(RG_CH), 0, s, w.buckets.as<uint32_t>(),
+                         w.bucket_start.as<uint32_t>(), d, pl.K, pl.nchunks, G, w.cross_key.as<uint32_t>(),
+                         w.lead_val.as<uint32_t>(), w.red_G.as<uint32_t>());
+    }
+    const bool pairs = red1_pairs();
+    auto red1 = pl.L == 4    ? (pairs ? k_bucket_reduce_1p<4> : k_bucket_reduce_1<4>)
+                : pl.L == 9  ? (pairs ? k_bucket_reduce_1p<9> : k_bucket_reduce_1<9>)
+                : pl.L == 10 ? (pairs ? k_bucket_reduce_1p<10> : k_bucket_reduce_1<10>)
+                : pl.L == 12 ? (pairs ? k_bucket_reduce_1p<12> : k_bucket_reduce_1<12>)
+                : pl.L == 16 ? (pairs ? k_bucket_reduce_1p<16> : k_bucket_reduce_1<16>)
+                : pl.L == 17 ? (pairs ? k_bucket_reduce_1p<17> : k_bucket_reduce_1<17>)
+                : pl.L == 20 ? (pairs ? k_bucket_reduce_1p<20> : k_bucket_reduce_1<20>)
+                             : (pairs ? k_bucket_reduce_1p<8> : k_bucket_reduce_1<8>);
+    if (!fold)
+    hipLaunchKernelGGL(red1, dim3(grid_for((size_t)d.W * pl.nchunks * (pairs ? 2 : 1), RED1_THREADS)), dim3(RED1_THREADS), 0, s,
                        w.buckets.as<uint32_t>(), w.bucket_start.as<uint32_t>(), d, pl.K, pl.nchunks,
                        w.cross_key.as<uint32_t>(), w.lead_val.as<uint32_t>(), w.red_U.as<uint32_t>(),
                        w.red_T.as<uint32_t>());
     mark(PH_RED1);
     if (red2_tree(pl)) {
       const uint32_t G = red2_groups(pl);
-      hipLaunchKernelGGL(k_red2_groups, dim3(d.W * G), dim3(4 * RG_CH), 0, s, w.red_U.as<uint32_t>(),
-                         w.red_T.as<uint32_t>(), pl.nchunks, G, w.bucket_start.as<uint32_t>(), d.B,
-                         w.red_G.as<uint32_t>());
+      if (!fold)
+        hipLaunchKernelGGL(k_red2_groups, dim3(d.W * G), dim3(4 * RG_CH), 0, s, w.red_U.as<uint32_t>(),
+                           w.red_T.as<uint32_t>(), pl.nchunks, G, w.bucket_start.as<uint32_t>(), d.B,
+                           w.red_G.as<uint32_t>());
       // one lane quad per group point of the widest term (a wave at least): 2^16 pipelined
       // 0.117-0.120 against 0.125-0.131 ms per MSM with 64 quads throughout
       uint32_t gp = 16;

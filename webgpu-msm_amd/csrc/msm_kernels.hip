@@ -1264,8 +1264,10 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
                                          uint32_t* __restrict__ g_tkey) {
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
   __shared__ uint32_t sh_hkey[ACC_THREADS];
+  PROBE(3, blockIdx.x, 0);
   acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets,
            lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
+  PROBE(3, blockIdx.x, 7);
 }
 
 // Joins for workgroups that k_accumulate found to hold a pass-through run (skewed scalars).
@@ -1453,16 +1455,13 @@ __device__ __forceinline__ bool red1_lane(const MsmDims& d, uint32_t L, uint32_t
   return false;
 }
 
+// Running sums of chunk c of window w (one lane): U = sum_i (i+1) B_i and T = sum_i B_i over the
+// chunk's buckets, i counted within the chunk.
 template <uint32_t RL>
-__global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
-                                                         const uint32_t* __restrict__ bucket_start, MsmDims d,
-                                                         uint32_t K, uint32_t nchunks,
-                                                         const uint32_t* __restrict__ cross_key,
-                                                         const uint32_t* __restrict__ lead_val,
-                                                         uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
-  uint32_t w, c;
-  if (!red1_lane(d, RL, nchunks, blockIdx.x * blockDim.x + threadIdx.x, w, c)) return;
-  const uint32_t g = w * nchunks + c;
+__device__ __forceinline__ void red1_chunk(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bucket_start,
+                                           const MsmDims& d, uint32_t K, uint32_t w, uint32_t c,
+                                           const uint32_t* __restrict__ cross_key, const uint32_t* __restrict__ lead_val,
+                                           xyzt& U, xyzt& T) {
   const uint32_t key0 = w * d.B + c * RL;
   const uint32_t nb = min(RL, d.B - c * RL);  // buckets of this chunk inside the window (last chunk: fewer)
   // bucket metadata up front (independent loads): which buckets are non-empty, and which left
@@ -1479,9 +1478,7 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
     }
   }
   if (!live) {  // whole chunk empty (e.g. the windows above the scalars' top bit)
-    const xyzt id = pt_identity();
-    store_pt(out_U + (size_t)g * PT_WORDS, id);
-    store_pt(out_T + (size_t)g * PT_WORDS, id);
+    U = T = pt_identity();
     return;
   }
   xyzt carry = pt_identity(), acc = pt_identity();
@@ -1509,8 +1506,99 @@ __global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t
       acc_live = true;
     }
   }
-  store_pt(out_U + (size_t)g * PT_WORDS, acc);
-  store_pt(out_T + (size_t)g * PT_WORDS, carry);
+  U = acc;
+  T = carry;
+}
+
+template <uint32_t RL>
+__global__ void __launch_bounds__(RED1_THREADS) k_bucket_reduce_1(const uint32_t* __restrict__ buckets,
+                                                         const uint32_t* __restrict__ bucket_start, MsmDims d,
+                                                         uint32_t K, uint32_t nchunks,
+                                                         const uint32_t* __restrict__ cross_key,
+                                                         const uint32_t* __restrict__ lead_val,
+                                                         uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
+  uint32_t w, c;
+  if (!red1_lane(d, RL, nchunks, blockIdx.x * blockDim.x + threadIdx.x, w, c)) return;
+  const uint32_t g = w * nchunks + c;
+  xyzt U, T;
+  red1_chunk<RL>(buckets, bucket_start, d, K, w, c, cross_key, lead_val, U, T);
+  store_pt(out_U + (size_t)g * PT_WORDS, U);
+  store_pt(out_T + (size_t)g * PT_WORDS, T);
+}
+
+// The same running sums on lane pairs (MSM_RED1_PAIRS=1; measured no faster, kept off): a chunk's two chains run on two
+// lanes in lock step -- the even lane the bucket chain T (carry += B_i, top bucket down), the odd
+// lane the weighted chain U (acc += the carry after the even lane's previous step, taken with a
+// DPP quad permute) -- so every lane holds one running point instead of two plus the prefetched
+// bucket: half the registers (more waves per SIMD to hide the adds' latency) for L + 1 steps of
+// one add instead of 2L adds.  Identity adds (empty buckets, the chains' ends) are harmless: the
+// formulas are complete.
+__device__ __forceinline__ fe fe_from_even(const fe& a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xA0, 0xF, 0xF, false);
+  return r;
+}
+
+#ifndef MSM_RED1P_WAVES
+#define MSM_RED1P_WAVES 3  // waves per SIMD asked of the compiler (4: <= 128 VGPRs, 17 spilled)
+#endif
+template <uint32_t RL>
+__global__ void __launch_bounds__(RED1_THREADS, MSM_RED1P_WAVES) k_bucket_reduce_1p(const uint32_t* __restrict__ buckets,
+                                                          const uint32_t* __restrict__ bucket_start, MsmDims d,
+                                                          uint32_t K, uint32_t nchunks,
+                                                          const uint32_t* __restrict__ cross_key,
+                                                          const uint32_t* __restrict__ lead_val,
+                                                          uint32_t* __restrict__ out_U, uint32_t* __restrict__ out_T) {
+  const bool u_lane = (threadIdx.x & 1u) != 0;
+  uint32_t w, c;
+  // both lanes of a pair map to the same chunk, so a pair leaves (or stays) together
+  if (!red1_lane(d, RL, nchunks, (blockIdx.x * blockDim.x + threadIdx.x) >> 1, w, c)) return;
+  const uint32_t g = w * nchunks + c;
+  const uint32_t key0 = w * d.B + c * RL;
+  const uint32_t nb = min(RL, d.B - c * RL);
+  uint32_t live = 0, cross = 0;
+  {
+    uint32_t bs[RL + 1];
+#pragma unroll
+    for (uint32_t i = 0; i <= RL; i++) bs[i] = i <= nb ? bucket_start[key0 + i] : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < RL; i++) {
+      if (i < nb && bs[i + 1] != bs[i]) {
+        live |= 1u << i;
+        if (!u_lane && cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
+      }
+    }
+  }
+  uint32_t* out = (u_lane ? out_U : out_T) + (size_t)g * PT_WORDS;
+  if (!live) {  // whole chunk empty (e.g. the windows above the scalars' top bit)
+    store_pt(out, pt_identity());
+    return;
+  }
+  const int top = 31 - __builtin_clz(live);
+  xyzt run = pt_identity();
+#pragma unroll 1
+  for (int i = top; i >= -1; i--) {
+    // the odd lane's operand: its even lane's carry as it stands before this step's add
+    xyzt q;
+    q.X = fe_from_even(run.X);
+    q.Y = fe_from_even(run.Y);
+    q.T = fe_from_even(run.T);
+    q.Z = fe_from_even(run.Z);
+    if (u_lane) {
+      // q as permuted (identity at the first step: the even lane's carry starts there)
+    } else if (i >= 0 && ((live >> i) & 1u)) {
+      q = load_pt(buckets + (size_t)(key0 + i) * PT_WORDS);
+      if ((cross >> i) & 1u) {  // rare: the bucket continues past its accumulation workgroup
+        const uint32_t g0 = (bucket_start[key0 + i] / K) / ACC_THREADS;
+        q = pt_add(q, load_pt(lead_val + (size_t)(g0 + 1) * PT_WORDS));
+      }
+    } else {
+      q = pt_identity();
+    }
+    run = pt_add(run, q);
+  }
+  store_pt(out, run);
 }
 
 // One workgroup per (window, term).  Terms 0..nv-1: R_{V,v} = sum of U_c over the v-th slice of
@@ -1651,30 +1739,17 @@ __device__ __forceinline__ fe load_fe_g(const uint32_t* __restrict__ src) {
   return a;
 }
 
-// One group's reduction (k_red2_groups): chunks g RG_CH .. of window w from
-// in_U / in_T into shA (T) / shB (U) and the RG_LOG steps; leaves V at shB[0], S at shA[0] and
-// R_k at shA[2^k].  Every thread of the block takes part (4 RG_CH threads, quad Q = chunk).
-__device__ __forceinline__ void red2_group_tree(const uint32_t* __restrict__ in_U, const uint32_t* __restrict__ in_T,
-                                                uint32_t nchunks, uint32_t w, uint32_t g,
-                                                uint32_t (*shA)[PT_WORDS], uint32_t (*shB)[PT_WORDS]) {
-  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
-  const uint32_t c = g * RG_CH + Q;
-  fe u, t;
-  if (c < nchunks) {
-    const size_t off = ((size_t)w * nchunks + c) * PT_WORDS + q * NL;
-    u = load_fe_g(in_U + off);
-    t = load_fe_g(in_T + off);
-  } else {
-    u = t = identity_coord(q);
-  }
-  store_fe_lds(&shB[Q][q * NL], u);
-  store_fe_lds(&shA[Q][q * NL], t);
-  __syncthreads();
+// The RG_LOG steps of one group's reduction over its chunk points in LDS (T in shA, U in shB):
+// leaves V at shB[0], S at shA[0] and R_k at shA[2^k].  Quad Q of the block's quads takes tasks
+// Q, Q + nquads, ... of each step (no task of a step reads another's destination).
+__device__ __forceinline__ void red2_tree_steps(uint32_t (*shA)[PT_WORDS], uint32_t (*shB)[PT_WORDS]) {
+  const uint32_t q = threadIdx.x & 3, nquads = blockDim.x >> 2;
 #pragma unroll 1
   for (uint32_t s = 0; s < RG_LOG; s++) {
     const uint32_t lp = RG_LOG - 1 - s;  // log2 of the pairs per list at this step
     const uint32_t ntask = (2 + s) << lp;
-    if (Q < ntask) {
+#pragma unroll 1
+    for (uint32_t Q = threadIdx.x >> 2; Q < ntask; Q += nquads) {
       const uint32_t kind = Q >> lp, i = Q & ((1u << lp) - 1u);
       uint32_t(*arr)[PT_WORDS] = kind == 1 ? shB : shA;
       uint32_t dst, srcx;
@@ -1692,6 +1767,28 @@ __device__ __forceinline__ void red2_group_tree(const uint32_t* __restrict__ in_
     }
     __syncthreads();
   }
+}
+
+// One group's reduction (k_red2_groups): chunks g RG_CH .. of window w from in_U / in_T into
+// shA (T) / shB (U), then the steps.  Every thread of the block takes part (4 RG_CH threads,
+// quad Q = chunk).
+__device__ __forceinline__ void red2_group_tree(const uint32_t* __restrict__ in_U, const uint32_t* __restrict__ in_T,
+                                                uint32_t nchunks, uint32_t w, uint32_t g,
+                                                uint32_t (*shA)[PT_WORDS], uint32_t (*shB)[PT_WORDS]) {
+  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const uint32_t c = g * RG_CH + Q;
+  fe u, t;
+  if (c < nchunks) {
+    const size_t off = ((size_t)w * nchunks + c) * PT_WORDS + q * NL;
+    u = load_fe_g(in_U + off);
+    t = load_fe_g(in_T + off);
+  } else {
+    u = t = identity_coord(q);
+  }
+  store_fe_lds(&shB[Q][q * NL], u);
+  store_fe_lds(&shA[Q][q * NL], t);
+  __syncthreads();
+  red2_tree_steps(shA, shB);
 }
 
 // Group point idx (0 V, 1 S, 2 + k R_k) of the tree left in shA / shB.
@@ -1763,6 +1860,83 @@ extern "C" __global__ void __launch_bounds__(4 * RG_CH) k_red2_groups(const uint
     uint32_t* o = out + (((size_t)w * ngroups + g) * RG_OUT + Q) * PT_WORDS + q * NL;
 #pragma unroll
     for (int k = 0; k < NL; k++) o[k] = v.v[k];
+  }
+}
+
+// The first stage and the group trees in one launch (MSM_RED_FOLD=1; measured slower, kept off:
+// the tree runs at the first stage's occupancy, two 226-VGPR waves per group): a workgroup of RG_CH
+// lanes takes one group of RG_CH consecutive chunks of a window -- each lane its chunk's running
+// sums (red1_chunk), straight into LDS, then the group's tree (red2_tree_steps, 32 quads) -- and
+// writes the group's V, S and R_0..R_{RG_LOG-1}: the chunk sums never go to memory and the second
+// launch of the stage (k_red2_groups) is gone.  Live groups first (red1_group), then the dead ones
+// (chunks a canonical scalar's digit cannot reach); a group without entries writes identities, and
+// an empty window's groups are not read.
+__device__ __forceinline__ bool red1_group(const MsmDims& d, uint32_t L, uint32_t nchunks, uint32_t G, uint32_t gd,
+                                           uint32_t& w, uint32_t& g, bool& live) {
+  uint32_t lg = 0;  // live groups per MSM
+  for (uint32_t l = 0; l < d.Wr; l++) lg += (red1_live_chunks(d, L, nchunks, d.w0 + l) + RG_CH - 1) / RG_CH;
+  const uint32_t dg = d.Wr * G - lg;
+  uint32_t r, m;
+  if (gd < d.nm * lg) {
+    m = gd / lg;
+    r = gd % lg;
+    live = true;
+  } else {
+    const uint32_t r0 = gd - d.nm * lg;
+    if (r0 >= d.nm * dg) return false;
+    m = r0 / dg;
+    r = r0 % dg;
+    live = false;
+  }
+  for (uint32_t l = 0; l < d.Wr; l++) {
+    const uint32_t lgl = (red1_live_chunks(d, L, nchunks, d.w0 + l) + RG_CH - 1) / RG_CH;
+    const uint32_t span = live ? lgl : G - lgl;
+    if (r < span) {
+      w = m * d.Wr + l;
+      g = live ? r : lgl + r;
+      return true;
+    }
+    r -= span;
+  }
+  return false;
+}
+
+template <uint32_t RL>
+__global__ void __launch_bounds__(RG_CH) k_bucket_reduce_1g(const uint32_t* __restrict__ buckets,
+                                                          const uint32_t* __restrict__ bucket_start, MsmDims d,
+                                                          uint32_t K, uint32_t nchunks, uint32_t ngroups,
+                                                          const uint32_t* __restrict__ cross_key,
+                                                          const uint32_t* __restrict__ lead_val,
+                                                          uint32_t* __restrict__ out) {
+  __shared__ uint32_t shA[RG_CH][PT_WORDS];  // T
+  __shared__ uint32_t shB[RG_CH][PT_WORDS];  // U
+  uint32_t w, g;
+  bool live;  // (order only: a dead group with entries is reduced like any other)
+  if (!red1_group(d, RL, nchunks, ngroups, blockIdx.x, w, g, live)) return;
+  if (bucket_start[(size_t)w * d.B] == bucket_start[(size_t)(w + 1) * d.B]) return;  // empty window: unread
+  uint32_t* o = out + ((size_t)w * ngroups + g) * RG_OUT * PT_WORDS;
+  // a group without entries (the dead groups, unless the scalars are non-canonical) is identities
+  const uint32_t kb0 = w * d.B + min(d.B, g * RG_CH * RL), kb1 = w * d.B + min(d.B, (g + 1) * RG_CH * RL);
+  if (bucket_start[kb0] == bucket_start[kb1]) {
+    for (uint32_t k = threadIdx.x; k < RG_OUT * 4; k += RG_CH) {
+      const fe id = identity_coord(k & 3);
+#pragma unroll
+      for (int j = 0; j < NL; j++) o[(k >> 2) * PT_WORDS + (k & 3) * NL + j] = id.v[j];
+    }
+    return;
+  }
+  const uint32_t c = g * RG_CH + threadIdx.x;
+  xyzt U = pt_identity(), T = pt_identity();
+  if (c < nchunks) red1_chunk<RL>(buckets, bucket_start, d, K, w, c, cross_key, lead_val, U, T);
+  store_pt_lds(shB[threadIdx.x], U);
+  store_pt_lds(shA[threadIdx.x], T);
+  __syncthreads();
+  red2_tree_steps(shA, shB);
+  const uint32_t Q = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (Q < RG_OUT) {
+    const fe v = load_fe_lds(red2_group_point(shA, shB, Q) + q * NL);
+#pragma unroll
+    for (int k = 0; k < NL; k++) o[Q * PT_WORDS + q * NL + k] = v.v[k];
   }
 }
 
