@@ -18,6 +18,8 @@
 #   batch64      the 64 x 2^18 prover batch (BASELINE configs[4])
 #   gloo8        the sharded bench with 8 gloo ranks on the one GPU (configs[3]'s shard shape)
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
+#   sharded      tools/sharded_probe.py: msm_compute's device-list path from host arrays, 1/2/8 shards
+#   rocprof20    rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 5 (exit status 0)
 #   split        per-GPU work of every points x windows split of a 2^20 MSM over 8 GPUs, on this one
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
 #   ktrace:VAR=A,B  kernel trace of the pipelined bench per value of one knob (tools/pipeline_timeline.py)
@@ -121,6 +123,10 @@ for step in "$@"; do
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 2 \
         --no-extras "${BENCH_Q[@]}" ;;
     multidev) run multidev 300 python bench.py --multi-device --no-extras "${BENCH_Q[@]}" ;;
+    sharded) run sharded 300 python tools/sharded_probe.py ;;  # the device-list host path, D repeated shards
+    rocprof20)  # the driver-shape bench (20 steps, 5 warm-up) under a kernel trace: must exit 0
+      run rocprof20 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_rocprof20_d" -o run \
+        -- python3 bench.py --steps 20 --warmup 5 ;;
     split) run split 600 python tools/split_probe.py --gpus 8 ;;
     split:*)  # split:D:SPLITS:C -- tools/split_probe.py over D GPUs for the listed PxQ splits at window width C
       IFS=: read -r _ ng sp cw <<< "$step"
