@@ -5,7 +5,8 @@
 //                        allocates; read in place by the addon)
 //   flat_copied_input_ms flat wire buffers over a plain ArrayBuffer (copied by the addon first)
 //   node_e2e_ms          U32ArrayPoint[] / Uint32Array[] objects (AllBenchmarks.tsx:81-94), with
-//                        marshal_ms = their JS flatten alone (flattenU32)
+//                        marshal_ms = their JS flatten alone into compute_msm's reused staging
+//                        (flattenStaged), marshal_fresh_ms = into fresh buffers (flattenU32)
 //   bigint_input_ms      BigIntPoint[] / bigint[] (the test-data loader's form, testCases.ts:34-52),
 //                        marshalled natively by the addon (napi_get_value_bigint_words)
 // The flat forms run first, on a fresh heap: millions of live point objects make V8's collector
@@ -18,7 +19,7 @@
 // them.  Prints one JSON line: medians and all run times (ms), and whether every result matched.
 import fs from "fs";
 import { performance } from "perf_hooks";
-import { compute_msm, flattenU32, u32ArrayToBigInts } from "../webgpu-msm_amd/js/submission.mjs";
+import { compute_msm, flattenStaged, flattenU32, releaseStaged, u32ArrayToBigInts } from "../webgpu-msm_amd/js/submission.mjs";
 
 const [, , pPath, sPath, nArg, runsArg, xArg, yArg] = process.argv;
 const n = parseInt(nArg, 10);
@@ -62,11 +63,14 @@ async function timeCalls(p, s) {
     scalars[i] = sw.slice(8 * i, 8 * i + 8);
   }
   const objTimes = await timeCalls(points, scalars);
-  const flat = [];
+  const flat = [], fresh = [];
   for (let r = 0; r < runs; r++) {
-    const t0 = performance.now();
-    flattenU32(points, scalars);
+    let t0 = performance.now();
+    releaseStaged(flattenStaged(points, scalars));  // what compute_msm does: reused staging
     flat.push(performance.now() - t0);
+    t0 = performance.now();
+    flattenU32(points, scalars);  // fresh SharedArrayBuffers (page faults on first touch)
+    fresh.push(performance.now() - t0);
   }
   points = scalars = null;
   // BigIntPoint[] / bigint[]
@@ -81,7 +85,7 @@ async function timeCalls(p, s) {
   const bigTimes = await timeCalls(bpoints, bscalars);
   console.log(JSON.stringify({
     flat_input_ms: med(flatTimes), flat_copied_input_ms: med(copyTimes), node_e2e_ms: med(objTimes),
-    marshal_ms: med(flat), bigint_input_ms: med(bigTimes), runs_ms: { flat: flatTimes, flat_copied: copyTimes,
+    marshal_ms: med(flat), marshal_fresh_ms: med(fresh), bigint_input_ms: med(bigTimes), runs_ms: { flat: flatTimes, flat_copied: copyTimes,
     objects: objTimes, bigint: bigTimes }, correct: expect ? ok : null,
   }));
 })().catch((e) => {

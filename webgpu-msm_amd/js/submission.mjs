@@ -61,6 +61,33 @@ export function flattenU32(points, scalars) {
   const n = Math.min(points.length, scalars.length);
   const pb = new Uint32Array(new SharedArrayBuffer(n * nUint32PerPoint * 4));
   const sb = new Uint32Array(new SharedArrayBuffer(n * nUint32PerScalar * 4));
+  flattenInto(points, scalars, n, pb, sb);
+  return [pb, sb];
+}
+
+// Staging buffers of compute_msm's object inputs, kept between calls: the first touch of fresh
+// SharedArrayBuffer pages costs ~50 ms per 160 MiB (2^20 points) in page faults, more than the
+// word copies.  A call takes a free pair (or makes one) and gives it back when its promise settles,
+// so concurrent calls never share one; at most two pairs of up to 2^21 points are kept.
+const stagingFree = [];
+function takeStaging(n) {
+  for (let i = 0; i < stagingFree.length; i++) if (stagingFree[i].cap >= n) return stagingFree.splice(i, 1)[0];
+  return { cap: n, pb: new Uint32Array(new SharedArrayBuffer(n * nUint32PerPoint * 4)),
+           sb: new Uint32Array(new SharedArrayBuffer(n * nUint32PerScalar * 4)) };
+}
+function giveStaging(st) {
+  if (st.cap <= 1 << 21 && stagingFree.length < 2) stagingFree.push(st);
+}
+// Exported for tools/node_e2e.mjs: compute_msm's marshalling of object inputs into reused staging.
+export function flattenStaged(points, scalars) {
+  const n = Math.min(points.length, scalars.length);
+  const st = takeStaging(n);
+  flattenInto(points, scalars, n, st.pb, st.sb);
+  return { st, pb: st.pb.subarray(0, n * nUint32PerPoint), sb: st.sb.subarray(0, n * nUint32PerScalar) };
+}
+export const releaseStaged = (staged) => giveStaging(staged.st);
+
+function flattenInto(points, scalars, n, pb, sb) {
   for (let i = 0; i < n; i++) {
     const p = points[i];
     const o = i * 32;
@@ -77,7 +104,6 @@ export function flattenU32(points, scalars) {
     sb[q] = s[0]; sb[q + 1] = s[1]; sb[q + 2] = s[2]; sb[q + 3] = s[3];
     sb[q + 4] = s[4]; sb[q + 5] = s[5]; sb[q + 6] = s[6]; sb[q + 7] = s[7];
   }
-  return [pb, sb];
 }
 
 function ratioFrom(options) {
@@ -114,8 +140,12 @@ export const compute_msm = async (baseAffinePoints, scalars, options) => {
     const sc = typeof scalars[0] === "bigint" ? scalars : scalars.map((s) => u32ArrayToBigInts(s)[0]);
     result = await addon.computeMsmBigInt(pts, sc, windowSize, devices, cpuWorkRatio);
   } else {
-    const [pointBuffer, scalarBuffer] = flattenU32(baseAffinePoints, scalars);
-    result = await addon.computeMsmU32(pointBuffer, scalarBuffer, windowSize, devices, cpuWorkRatio);
+    const staged = flattenStaged(baseAffinePoints, scalars);
+    try {
+      result = await addon.computeMsmU32(staged.pb, staged.sb, windowSize, devices, cpuWorkRatio);
+    } finally {
+      giveStaging(staged.st);
+    }
   }
   const [x, y] = u32ArrayToBigInts(result);
   return { x, y };
