@@ -209,7 +209,10 @@ int msm_compute_shared_device(const uint32_t* d_points_be, const uint32_t* const
  * scalar vectors.  Inputs are uploaded on a copy stream into the in-flight launch slots while the
  * other slots compute (the base vector of msm_compute_shared once, piece by piece, prepared as it
  * lands); msm_compute_many packs x|y of every point as msm_compute does (t checked on the host,
- * MSM_ERR_COORD_RANGE for t >= p).  Results [count][16]. */
+ * MSM_ERR_COORD_RANGE for t >= p).  Results [count][16].  Footprint: msm_compute_many's packing
+ * keeps three pinned host buffers of one launch's points and scalars (nm * n * 128 B each: nm = 2
+ * MSMs per launch up to 2^21 points, 4 up to 2^18, 8 up to 2^16 -- e.g. 3 x 256 MiB at 2^20) until
+ * msm_shutdown; a launch needing more than 512 MiB per buffer (MSM_PIN_MAX_MB) uploads unpacked. */
 int msm_compute_many(const uint32_t* const* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
                      const msm_opts* opts, uint32_t* out_xy_be);
 int msm_compute_shared(const uint32_t* points_be, const uint32_t* const* scalars_be, size_t n, size_t count,
