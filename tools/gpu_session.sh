@@ -20,6 +20,8 @@
 #   multidev     bench.py --multi-device: msm_compute over every visible device in one process
 #   sharded      tools/sharded_probe.py: msm_compute's device-list path from host arrays, 1/2/8 shards
 #   rocprof20    rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 5 (exit status 0)
+#   splitrl:K1,K2[:R]  the 4 x 2 shares over accumulation run lengths (0 = the plan's)
+#   splitk       one-stream kernel trace of the 4 x 2 (c = 15) shares of an 8-GPU split
 #   split        per-GPU work of every points x windows split of a 2^20 MSM over 8 GPUs, on this one
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
 #   ktrace:VAR=A,B  kernel trace of the pipelined bench per value of one knob (tools/pipeline_timeline.py)
@@ -128,9 +130,19 @@ for step in "$@"; do
       run rocprof20 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_rocprof20_d" -o run \
         -- python3 bench.py --steps 20 --warmup 5 ;;
     split) run split 600 python tools/split_probe.py --gpus 8 ;;
+    splitrl:*)  # splitrl:K1,K2[:R] -- the 4 x 2 (c = 15) shares of an 8-GPU split over accumulation run lengths
+      IFS=: read -r _ ks rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for k in ${ks//,/ }; do
+          run "splitrl_k${k}_$r" 300 python tools/split_probe.py --gpus 8 --splits 4x2 --window 15 --run-length "$k"
+        done
+      done ;;
     split:*)  # split:D:SPLITS:C -- tools/split_probe.py over D GPUs for the listed PxQ splits at window width C
       IFS=: read -r _ ng sp cw <<< "$step"
       run "split${ng}_${sp//,/_}_c${cw}${KS:-}" 600 python tools/split_probe.py --gpus "$ng" --splits "$sp" --window "$cw" ;;
+    splitk)  # one-stream kernel trace of the 8-GPU 4 x 2 (c = 15) shares, each virtual GPU in turn
+      MSM_SLOTS=1 MSM_FORK_PREP=0 run "splitk${KS:-}" 300 rocprofv3 --kernel-trace --output-format csv \
+        -d "gpurun_out/${TAG}_splitk${KS:-}_d" -o run -- python3 tools/split_probe.py --gpus 8 --splits 4x2 --window 15 ;;
     kstats)
       run kstats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kstats_d -o run \
         -- python3 bench.py ;;

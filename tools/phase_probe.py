@@ -6,6 +6,7 @@ launch span, the workgroups' mean lifetime, how many were resident on average, a
 median / p90 duration.
 
     MSM_SLOTS=1 MSM_AMD_LIB=.../libmsm_probe.so python tools/phase_probe.py [--n 1048576]
+    (one 8-GPU share: --n 262144 --count 4 --window 15 --split-q 2 --wrange 0)
 """
 import argparse
 import ctypes
@@ -40,6 +41,9 @@ def analyse(raw):
         ghz = float(np.median(cyc / np.maximum(life_us, 1e-3) / 1e3))
         rec = {"workgroups": int(len(live)), "span_us": round(float(span_us), 2),
                "life_us_mean": round(float(life_us.mean()), 3), "life_us_p90": round(float(np.percentile(life_us, 90)), 3),
+               "life_us_pct": {str(q): round(float(np.percentile(life_us, q)), 2) for q in (1, 10, 50, 90, 99, 100)},
+               "end_us_pct": {str(q): round(float(np.percentile((rt1 - rt0.min()) / 100.0, q)), 2)
+                              for q in (1, 10, 50, 90, 99, 100)},
                "resident_mean": round(float(life_us.sum() / span_us), 1), "clock_ghz": round(ghz, 3), "phases": {}}
         prev = 0
         for s in sorted(phases):
@@ -63,6 +67,10 @@ def main():
     ap.add_argument("--count", type=int, default=2)
     ap.add_argument("--runs", type=int, default=6)
     ap.add_argument("--out", default="gpurun_out/phase_probe.bin")
+    ap.add_argument("--window", type=int, default=0, help="window width (0: the plan's)")
+    ap.add_argument("--split-q", type=int, default=0,
+                    help="run one share of a points x Q window split: Q window ranges at half windows")
+    ap.add_argument("--wrange", type=int, default=0, help="which of the Q window ranges (with --split-q)")
     args = ap.parse_args()
     import torch
 
@@ -74,8 +82,14 @@ def main():
     pts = [torch.from_numpy(M.gen_points(args.n).view(np.int32)).to(dev) for _ in range(1)] * args.count
     scs = [torch.from_numpy(M.gen_scalars(args.n, seed=17 + i).view(np.int32)).to(dev) for i in range(args.count)]
     torch.cuda.synchronize()
-    for _ in range(args.runs):
-        M.compute_msm_many_device(pts, scs, args.n)
+    if args.split_q:
+        from msm_amd.dist import SPLIT_HALF_WINDOWS, window_ranges
+        r = window_ranges(M.window_count(args.window), args.split_q, SPLIT_HALF_WINDOWS)[args.wrange]
+        for _ in range(args.runs):
+            M.compute_msm_many_device_partial(pts, scs, args.n, window_size=args.window or None, windows=r)
+    else:
+        for _ in range(args.runs):
+            M.compute_msm_many_device(pts, scs, args.n, window_size=args.window or None)
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     rc = L.msm_test_probe_dump(args.out.encode())
     assert rc == 0, rc

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--window", type=int, default=0, help="window width for the window-split runs (0: 16)")
     ap.add_argument("--splits", default="", help="comma-separated PxQ (default: every factorisation of --gpus)")
+    ap.add_argument("--run-length", type=int, default=0, help="accumulation run length K (0: the plan's)")
     ap.add_argument("--whole-windows", action="store_true",
                     help="cut the window ranges at whole windows (default: half windows, as split_part)")
     a = ap.parse_args()
@@ -65,7 +66,8 @@ def main():
             torch.cuda.synchronize()
             for r in ranges:
                 run = lambda k: M.compute_msm_many_device_partial(  # noqa: E731
-                    [d_pts] * k, [d_sc[j] for j in js[:k]], hi - lo, window_size=c or None, windows=r)
+                    [d_pts] * k, [d_sc[j] for j in js[:k]], hi - lo, window_size=c or None, windows=r,
+                    run_length=a.run_length or None)
                 run(a.warmup)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -79,6 +81,7 @@ def main():
         ok = all(e is None or g == e for g, e in zip(joined, [exp[j] for j in js]))
         worst = max(g["ms_per_msm"] for g in per_gpu)
         line = {"split": f"{P}x{Q}", "gpus": D, "n": n, "window_bits": c or "auto", "steps": K,
+                "run_length": a.run_length or "plan",
                 "per_gpu_ms_per_msm_max": worst,
                 "per_gpu_ms_per_msm_mean": round(float(np.mean([g["ms_per_msm"] for g in per_gpu])), 4),
                 "correct": ok, "virtual_gpus": per_gpu}
