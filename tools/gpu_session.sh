@@ -21,6 +21,7 @@
 #   sharded      tools/sharded_probe.py: msm_compute's device-list path from host arrays, 1/2/8 shards
 #   rocprof20    rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 5 (exit status 0)
 #   splitrl:K1,K2[:R]  the 4 x 2 shares over accumulation run lengths (0 = the plan's)
+#   splitlib:LIBS[:R]  the 4 x 2 shares for each in-tree library variant
 #   splitk       one-stream kernel trace of the 4 x 2 (c = 15) shares of an 8-GPU split
 #   split        per-GPU work of every points x windows split of a 2^20 MSM over 8 GPUs, on this one
 #   kstats       rocprofv3 --kernel-trace --stats of the default bench command
@@ -140,6 +141,13 @@ for step in "$@"; do
     split:*)  # split:D:SPLITS:C -- tools/split_probe.py over D GPUs for the listed PxQ splits at window width C
       IFS=: read -r _ ng sp cw <<< "$step"
       run "split${ng}_${sp//,/_}_c${cw}${KS:-}" 600 python tools/split_probe.py --gpus "$ng" --splits "$sp" --window "$cw" ;;
+    splitlib:*)  # splitlib:LIBS[:R] -- the 4 x 2 (c = 15) shares of an 8-GPU split for each in-tree library variant
+      IFS=: read -r _ libs rounds <<< "$step"
+      for r in $(seq 1 "${rounds:-2}"); do
+        for lib in ${libs//,/ }; do
+          MSM_AMD_LIB=$LIBDIR/$lib run "splitlib_${lib%.so}_$r" 300 python tools/split_probe.py --gpus 8 --splits 4x2 --window 15
+        done
+      done ;;
     splitk)  # one-stream kernel trace of the 8-GPU 4 x 2 (c = 15) shares, each virtual GPU in turn
       MSM_SLOTS=1 MSM_FORK_PREP=0 run "splitk${KS:-}" 300 rocprofv3 --kernel-trace --output-format csv \
         -d "gpurun_out/${TAG}_splitk${KS:-}_d" -o run -- python3 tools/split_probe.py --gpus 8 --splits 4x2 --window 15 ;;

@@ -1111,6 +1111,17 @@ __device__ __forceinline__ uint32_t next_nonempty(const uint32_t* __restrict__ b
 #ifndef MSM_ACC_VEC
 #define MSM_ACC_VEC 1
 #endif
+// Progress-ordered wave priority.  A SIMD's VALU issue goes by wave priority, then age, so of the
+// four equal runs sharing a SIMD the oldest finished first and the youngest last (an 8-GPU share,
+// one round of workgroups: 186 / 294 / 407 / 510 us by dispatch order, tools/phase_probe.py), and
+// the last ~30% of the launch ran with one to three waves per SIMD.  Each wave therefore lowers
+// its priority as it passes each quarter of its run (3, 2, 1, 0): a wave ahead of its partners
+// yields to them, and the four finish within the last quarter's age order (share: 371 / 400 /
+// 428 / 453 us).  A lone 2^20 MSM's accumulation 744 -> 717 us (latency 1.074 -> 1.045 ms);
+// pipelined launches and the 8-GPU shares within noise (sessions t15, t16).
+#ifndef MSM_ACC_PRIO
+#define MSM_ACC_PRIO 1
+#endif
 constexpr uint32_t ACC_THREADS = 256;
 // One workgroup-sized tile of the accumulation: runs [wg ACC_THREADS, (wg + 1) ACC_THREADS).
 __device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WORDS], uint32_t* sh_hkey,
@@ -1149,7 +1160,20 @@ __device__ __forceinline__ void acc_tile(uint32_t wg, uint32_t (*sh_head)[PT_WOR
     const bool vec = (K & 3u) == 0;  // run starts (t K) are then 16-B aligned
     uint4 eb = make_uint4(0u, 0u, 0u, 0u);
 #endif
+#if MSM_ACC_PRIO
+    // (levels at 70 / 84 / 95% of the run instead, so that the age order left inside the last
+    // level decides only its last 5%: pipelined 2^20 +7%, session t16)
+    const uint32_t q1 = K >> 2, q2 = K >> 1, q3 = q1 + q2;
+#endif
     for (uint32_t pos = s; pos < e; pos++) {
+#if MSM_ACC_PRIO
+      {
+        const uint32_t q = __builtin_amdgcn_readfirstlane(pos - s);  // uniform: every run is K long
+        if (q == q1) __builtin_amdgcn_s_setprio(2);
+        else if (q == q2) __builtin_amdgcn_s_setprio(1);
+        else if (q == q3) __builtin_amdgcn_s_setprio(0);
+      }
+#endif
 #if MSM_ACC_VEC
       const uint32_t jq = (pos - s) & 3u;  // uniform across the lanes still in the loop
       if (vec && jq == 0) eb = *reinterpret_cast<const uint4*>(sorted_entry + pos);
@@ -1265,6 +1289,9 @@ extern "C" __global__ void __launch_bounds__(ACC_THREADS) k_accumulate(const uin
   __shared__ uint32_t sh_head[ACC_THREADS][PT_WORDS];
   __shared__ uint32_t sh_hkey[ACC_THREADS];
   PROBE(3, blockIdx.x, 0);
+#if MSM_ACC_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
   acc_tile(blockIdx.x, sh_head, sh_hkey, pts, sorted_entry, bucket_start, run_key, total_ptr, K, nkeys, buckets,
            lead_val, lead_open, cross_key, skew_list, g_head, g_hkey, g_tkey);
   PROBE(3, blockIdx.x, 7);
