@@ -61,6 +61,7 @@ print(json.dumps(out))
     {"MSM_RED1_PAIRS": "1"},                       # first reduction stage on lane pairs
     {"MSM_RED_FOLD": "1"},                         # first stage and group trees in one launch
     {"MSM_RECODE_FIXED": "0"},                     # the generic recode loop at every width
+    {"MSM_STAGGER": "0"},                          # pipelined launches not staggered
 ])
 def test_knob_paths_bit_exact(env):
     e = dict(os.environ)

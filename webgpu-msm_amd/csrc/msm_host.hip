@@ -180,7 +180,7 @@ struct Segment {
   Plan pl{};
   int parts = 0;
   const uint32_t* pts_buf = nullptr;  // the point-record buffer the captured kernels use
-  bool acc_events = false;            // event-record nodes around k_accumulate
+  int acc_events = 0;                 // event-record nodes: 2 around k_accumulate, 1 after it only
   bool fork = false;                  // the preparation forked beside the sort (slot_forks)
   uint64_t gen = 0;
   uint64_t used = 0;
@@ -221,6 +221,7 @@ struct Slot {
   hipEvent_t ev_sc = nullptr;  // the scalars of the slot's next launch are in place (host uploads)
   Plan pl{};
   bool acc_timed = false;
+  bool stagger = false;  // this slot's pipelined launches are staggered (stagger_launches)
   bool pipelined = false;  // a launch of a pipelined run (another launch in flight beside it)
 };
 constexpr int NSLOT = 4;      // at most this many launches in flight (one HIP stream each)
@@ -725,10 +726,11 @@ bool is_recode_kernel(const void* f) {
 
 // Enqueue parts of the device pipeline on `s`; the reduced per-window terms land in the slot's
 // h_out.  `pts` is the point-record buffer (the slot's own, or a shared base vector's).
-// With `acc_events` (eager launches only), k_accumulate runs between the slot's ev_acc0 / ev_acc1;
+// With `acc_events` (eager launches only), k_accumulate runs between the slot's ev_acc0 / ev_acc1
+// (2), or is followed by ev_acc1 alone (1);
 // captured graphs get the same events as record nodes (add_acc_event_nodes).
 int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
-                hipStream_t s, int parts, uint32_t* pts, bool acc_events = false) {
+                hipStream_t s, int parts, uint32_t* pts, int acc_events = 0) {
   const MsmDims& d = pl.d;
   Slot& sl = c->slot[si];
   Workspace& w = sl.ws;
@@ -743,6 +745,10 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
   // graph) and rejoins before the accumulation, so a lone MSM's sort no longer waits behind it.
   // (Profiling mode 1 keeps them in order, one event between every phase.)
   const bool fork = (parts & PART_PREP) && (parts & PART_SORT) && !prof && slot_forks(sl);
+  auto prepare = [&](hipStream_t ps) {
+    hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, ps,
+                       d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n), pl.pfmt);
+  };
   if (parts & PART_PREP) {
     mark(PH_START);
     hipStream_t ps = s;
@@ -751,8 +757,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
       HIPCHECK(hipStreamWaitEvent(sl.aux, sl.ev_fork, 0));
       ps = sl.aux;
     }
-    hipLaunchKernelGGL(k_prepare_points, dim3(grid_for(d.n, PP_THREADS), d.shared ? 1 : d.nm), dim3(PP_THREADS), 0, ps,
-                       d_points, pts, d.n, w.err.as<uint32_t>(), prep_nt((size_t)(d.shared ? 1 : d.nm) * d.n), pl.pfmt);
+    prepare(ps);
     if (fork) HIPCHECK(hipEventRecord(sl.ev_join, sl.aux));
     mark(PH_PREPARE);
   }
@@ -786,7 +791,7 @@ int enqueue_msm(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const Batc
     mark(PH_FINE);
   }
   if (fork) HIPCHECK(hipStreamWaitEvent(s, sl.ev_join, 0));
-  if ((parts & PART_ACC) && acc_events) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
+  if ((parts & PART_ACC) && acc_events == 2) HIPCHECK(hipEventRecord(sl.ev_acc0, s));
   if (parts & PART_ACC) {
     hipLaunchKernelGGL(k_accumulate, dim3(rgrid), dim3(ACC_THREADS), 0, s, pts, w.sorted_entry.as<uint32_t>(),
                        w.bucket_start.as<uint32_t>(), w.run_key.as<uint32_t>(), total, pl.K, d.W * d.B,
@@ -1412,7 +1417,7 @@ bool graphs_enabled() {
 
 // Bracket the captured k_accumulate node with event-record nodes (the slot's ev_acc0 / ev_acc1):
 // every replay of the graph then times the accumulation, with no extra launches.
-int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
+int add_acc_event_nodes(hipGraph_t g, Slot& sl, bool both) {
   size_t num = 0;
   if (hipGraphGetNodes(g, nullptr, &num) != hipSuccess || num == 0) return MSM_ERR_HIP;
   std::vector<hipGraphNode_t> nodes(num);
@@ -1436,11 +1441,13 @@ int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
       (nx && hipGraphNodeGetDependentNodes(acc, outs.data(), &nx) != hipSuccess))
     return MSM_ERR_HIP;
   hipGraphNode_t r0 = nullptr, r1 = nullptr;
-  for (hipGraphNode_t d : deps)
-    if (hipGraphRemoveDependencies(g, &d, &acc, 1) != hipSuccess) return MSM_ERR_HIP;
-  if (hipGraphAddEventRecordNode(&r0, g, deps.data(), deps.size(), sl.ev_acc0) != hipSuccess ||
-      hipGraphAddDependencies(g, &r0, &acc, 1) != hipSuccess)
-    return MSM_ERR_HIP;
+  if (both) {
+    for (hipGraphNode_t d : deps)
+      if (hipGraphRemoveDependencies(g, &d, &acc, 1) != hipSuccess) return MSM_ERR_HIP;
+    if (hipGraphAddEventRecordNode(&r0, g, deps.data(), deps.size(), sl.ev_acc0) != hipSuccess ||
+        hipGraphAddDependencies(g, &r0, &acc, 1) != hipSuccess)
+      return MSM_ERR_HIP;
+  }
   for (hipGraphNode_t o : outs)
     if (hipGraphRemoveDependencies(g, &acc, &o, 1) != hipSuccess) return MSM_ERR_HIP;
   if (hipGraphAddEventRecordNode(&r1, g, &acc, 1, sl.ev_acc1) != hipSuccess) return MSM_ERR_HIP;
@@ -1450,7 +1457,7 @@ int add_acc_event_nodes(hipGraph_t g, Slot& sl) {
 }
 
 int capture(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si, hipStream_t s,
-            int parts, uint32_t* pts, bool acc_events, hipGraph_t* gout, hipGraphExec_t* out) {
+            int parts, uint32_t* pts, int acc_events, hipGraph_t* gout, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return MSM_ERR_HIP;
   int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts);
@@ -1460,7 +1467,7 @@ int capture(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtr
     (void)hipGetLastError();
     return MSM_ERR_HIP;
   }
-  if (acc_events && (parts & PART_ACC) && add_acc_event_nodes(g, c->slot[si]) != MSM_OK) {
+  if (acc_events && (parts & PART_ACC) && add_acc_event_nodes(g, c->slot[si], acc_events == 2) != MSM_OK) {
     hipGraphDestroy(g);
     (void)hipGetLastError();
     return MSM_ERR_HIP;
@@ -1539,7 +1546,7 @@ int repoint_inputs(const Plan& pl, Slot& sl, Segment& sg, const BatchPtrs& d_poi
 // The cached graph of `parts` for this plan (captured on first use, least recently used segment
 // evicted), repointed at the launch's inputs; nullptr when graphs are unavailable.
 Segment* get_segment(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchPtrs& d_scalars, int si,
-                     int parts, uint32_t* pts, bool acc_events) {
+                     int parts, uint32_t* pts, int acc_events) {
   Slot& sl = c->slot[si];
   const uint64_t gen = g_alloc_gen.load();
   Segment* hit = nullptr;
@@ -1598,8 +1605,9 @@ int launch_on(DevCtx* c, const Plan& pl, const BatchPtrs& d_points, const BatchP
               uint32_t* pts, hipStream_t s) {
   // k_accumulate's bracketing events only when profiling mode 2 reads them: each event-record
   // node adds ~6 us to the launch sequence's critical path (profiles/r3/latency_timeline.txt)
-  const bool acc = (parts & PART_ACC) != 0 && c->profiling == 2;
-  if (parts & PART_ACC) c->slot[si].acc_timed = acc;
+  // (a staggered slot's graphs also record ev_acc1 after k_accumulate: the next launch waits on it)
+  const int acc = (parts & PART_ACC) == 0 ? 0 : c->profiling == 2 ? 2 : c->slot[si].stagger ? 1 : 0;
+  if (parts & PART_ACC) c->slot[si].acc_timed = acc == 2;
   if (c->profiling == 1) {
     c->slot[si].acc_timed = false;
     if (int rc = enqueue_msm(c, pl, d_points, d_scalars, si, s, parts, pts)) return rc;
@@ -1797,6 +1805,7 @@ int run_device(DevCtx* c, const uint32_t* d_points, const uint32_t* d_scalars, s
   if (rc != MSM_OK) return rc;
   const int si = 0;  // a lone MSM always uses slot 0 (the other workspaces only for pipelining)
   c->slot[si].pipelined = false;
+  c->slot[si].stagger = false;
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = order_after_user(c, user_stream, 1)) != MSM_OK) return rc;
   c->slot[si].pl = pl;
@@ -1863,6 +1872,7 @@ int run_host(DevCtx* c, const uint32_t* points_be, const uint32_t* scalars_be, s
   const int si = 0;
   Slot& sl = c->slot[si];
   sl.pipelined = false;
+  sl.stagger = false;
   Workspace& w = sl.ws;
   if ((rc = ensure_workspace(c, pl, si)) != MSM_OK) return rc;
   if ((rc = w.wire_pts.ensure(n * 128)) != MSM_OK || (rc = w.wire_sc.ensure(n * 32)) != MSM_OK) return rc;
@@ -1972,6 +1982,19 @@ uint32_t pipeline_batch(size_t n, size_t count) {
 // upload (MSM_HOST_SORT_EARLY=0 disables, for A/B runs).
 bool host_sort_early() {
   static const bool on = !(getenv("MSM_HOST_SORT_EARLY") && atoi(getenv("MSM_HOST_SORT_EARLY")) == 0);
+  return on;
+}
+
+// Staggered pipelined launches (default; MSM_STAGGER=0 turns them off): launch j's preparation and
+// sort wait for launch j-1's accumulation -- the stream waits on the previous slot's ev_acc1,
+// recorded by an event node right after k_accumulate inside that launch's graph -- so they run
+// beside j-1's bucket reduction (one wave per SIMD, no LDS) instead of being dispatched into the
+// accumulation that holds every CU.  Unstaggered, the two slots drifted into running their
+// accumulations side by side and their sorts and reductions side by side (kernel traces t11,
+// t19); staggered, 2^20 pipelined 0.966-0.973 against 0.985-1.013 ms per MSM (sessions t20-t23,
+// DESIGN.md §4.1).  Device-resident inputs only: host-input launches are paced by their uploads.
+bool stagger_launches() {
+  static const bool on = !(getenv("MSM_STAGGER") && atoi(getenv("MSM_STAGGER")) == 0);
   return on;
 }
 
@@ -2273,6 +2296,8 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // runs after j is enqueued, so the device holds nslot launches while the host works
   // (otherwise launches that finish together leave the device idle for a Horner each).
   std::vector<uint32_t> terms;
+  const bool stagger = nslot > 1 && !host && c->profiling != 1 && stagger_launches();
+  for (int si = 0; si < NSLOT; si++) c->slot[si].stagger = stagger && si < nslot;
   for (size_t j = 0; j < nbatch + nslot; j++) {
     const bool have = j >= (size_t)nslot;
     const size_t f = have ? j - nslot : 0;
@@ -2304,8 +2329,11 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
       Plan plj = pl;
       plj.pfmt = packed ? launch_fmt[j] : PT_FMT_WIRE;  // set by the uploader before up_ready
       sl.pl = plj;
-      if ((rc = launch_parts(c, plj, bp, bs, si, sort_early ? parts & ~PART_SORT : parts, pts)) != MSM_OK)
-        return fail(rc);
+      const int lp = sort_early ? parts & ~PART_SORT : parts;
+      // staggered: launch j's preparation and sort after launch j-1's accumulation
+      if (stagger && j > 0 && hipStreamWaitEvent(sl.stream, c->slot[(j - 1) % nslot].ev_acc1, 0) != hipSuccess)
+        return fail(MSM_ERR_HIP);
+      if ((rc = launch_parts(c, plj, bp, bs, si, lp, pts)) != MSM_OK) return fail(rc);
       enqueued.store(j + 1, std::memory_order_release);
       if (crew && j + 1 == nbatch) {
         crew->arm();  // spins while the device runs the last launch
