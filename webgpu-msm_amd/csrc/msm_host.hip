@@ -1993,9 +1993,10 @@ bool host_sort_early() {
 // accumulations side by side and their sorts and reductions side by side (kernel traces t11,
 // t19); staggered, 2^20 pipelined 0.966-0.973 against 0.985-1.013 ms per MSM (sessions t20-t23,
 // DESIGN.md §4.1).  Device-resident inputs only: host-input launches are paced by their uploads.
-bool stagger_launches() {
-  static const bool on = !(getenv("MSM_STAGGER") && atoi(getenv("MSM_STAGGER")) == 0);
-  return on;
+// (MSM_STAGGER=2 staggers host-input launches too, for A/B runs.)
+int stagger_launches() {
+  static const int v = getenv("MSM_STAGGER") ? atoi(getenv("MSM_STAGGER")) : 1;
+  return v < 0 ? 0 : v > 2 ? 2 : v;
 }
 
 // Where the inputs of one pipelined run come from.
@@ -2296,7 +2297,7 @@ int run_many(DevCtx* c, const ManyInputs& in, size_t n, size_t count, const msm_
   // runs after j is enqueued, so the device holds nslot launches while the host works
   // (otherwise launches that finish together leave the device idle for a Horner each).
   std::vector<uint32_t> terms;
-  const bool stagger = nslot > 1 && !host && c->profiling != 1 && stagger_launches();
+  const bool stagger = nslot > 1 && c->profiling != 1 && stagger_launches() > (host ? 1 : 0);
   for (int si = 0; si < NSLOT; si++) c->slot[si].stagger = stagger && si < nslot;
   for (size_t j = 0; j < nbatch + nslot; j++) {
     const bool have = j >= (size_t)nslot;
