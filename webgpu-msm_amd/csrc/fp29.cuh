@@ -456,13 +456,11 @@ __device__ __forceinline__ fe fe_to_mont(const fe& std_limbs) { return fe_mul(st
 __device__ __forceinline__ bool words_lt_p(const uint32_t w[8]) {
   const uint32_t PW[8] = {0x00000001u, 0x0a118000u, 0xd0000001u, 0x59aa76feu,
                           0x5c37b001u, 0x60b44d1eu, 0x9a2ca556u, 0x12ab655eu};
-  bool lt = false, eq = true;
+  // w < p iff w - p borrows: one subtract-with-borrow per word (v_sub_co / v_subb_co)
+  unsigned int b = 0;
 #pragma unroll
-  for (int i = 7; i >= 0; i--) {
-    lt = lt || (eq && w[i] < PW[i]);
-    eq = eq && (w[i] == PW[i]);
-  }
-  return lt;
+  for (int i = 0; i < 8; i++) (void)__builtin_subc(w[i], PW[i], b, &b);
+  return b != 0;
 }
 
 // Inverse by Fermat (a^(p-2)); only used on the rare z != 1 input path.

@@ -90,6 +90,7 @@ __device__ __forceinline__ fe load_fe(const uint32_t* src) {
 #define MSM_PP_THREADS 256
 #endif
 constexpr uint32_t PP_THREADS = MSM_PP_THREADS;
+static_assert(PP_THREADS * 8 <= (1u << 16), "k_prepare_points' multiply-high slot division");
 typedef uint32_t pp_v4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t pp_slot(uint32_t rec, uint32_t q) { return rec * 8 + (q ^ (rec & 7)); }
 
@@ -113,6 +114,9 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
                                                                           uint32_t fmt) {
   __shared__ uint4 st[PP_THREADS * 8];
   const uint32_t S = pt_fmt_slots(fmt);
+  // g / S for the wave-uniform S in {4, 6, 8} as one multiply-high (exact for g < 2^16; the
+  // generic unsigned division it replaces cost ~12 VALU per slot)
+  const uint32_t s_inv = S == 8 ? (1u << 29) : S == 4 ? (1u << 30) : 0x2AAAAAABu;
   const uint32_t p0 = blockIdx.x * PP_THREADS;
   const uint32_t np = min(PP_THREADS, n - p0);
   const uint4* src = reinterpret_cast<const uint4*>(wires.p[blockIdx.y]) + (size_t)p0 * S;
@@ -120,7 +124,8 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
     const uint32_t g = j * PP_THREADS + threadIdx.x;  // 16-B slot within the block's records
-    if (g < np * S) st[pp_slot(g / S, g % S)] = src[g];
+    const uint32_t rec = __umulhi(g, s_inv);
+    if (g < np * S) st[pp_slot(rec, g - rec * S)] = src[g];
   }
   __syncthreads();
   const uint32_t i = threadIdx.x;
