@@ -824,6 +824,13 @@ __device__ __forceinline__ void part_load(const uint32_t* __restrict__ pe, const
   }
 }
 
+// floor(x / D) for a runtime, wave-uniform D, given inv = 1.0 / D: (x + 0.5) / D is at least
+// 0.5 / D away from an integer, and the two roundings (inv, the product) err by < 2^-20 / D for any
+// 32-bit x, so the truncation is exact.  Three VALU against the ~14 of an unsigned division.
+__device__ __forceinline__ uint32_t div_by_inv(uint32_t x, double inv) {
+  return (uint32_t)(((double)x + 0.5) * inv);
+}
+
 __device__ __forceinline__ void count_runs(uint32_t* cnt, uint32_t& last, uint32_t& run, uint32_t key) {
   if (key == last) {
     run++;
@@ -948,6 +955,7 @@ extern "C" __global__ void FS_BOUNDS k_fine_sort(const uint32_t* __restrict__ pa
   // per-bucket counts -> exclusive offsets; boundaries and run starts go out with them (a bucket
   // ends where the next one starts)
   lds_excl_scan_wave0(cnt, nf);
+  const double kinv = 1.0 / (double)K;  // div_by_inv: the bucket's first run, ceil(gs / K)
   __syncthreads();
   PROBE(2, bin, 4);
 #pragma unroll
@@ -957,7 +965,8 @@ extern "C" __global__ void FS_BOUNDS k_fine_sort(const uint32_t* __restrict__ pa
       const uint32_t gs = base + cnt[f];
       const uint32_t ge = base + (f + 1 < nf ? cnt[f + 1] : m);
       bucket_start[key0 + f] = gs;
-      for (uint32_t r = (gs + K - 1) / K; r * K < ge; r++) run_key[r] = key0 + f;
+      const uint32_t r0 = div_by_inv(gs + K - 1, kinv);
+      for (uint32_t r = r0; r * K < ge; r++) run_key[r] = key0 + f;
     }
   }
   __syncthreads();
@@ -1502,11 +1511,12 @@ __device__ __forceinline__ void red1_chunk(const uint32_t* __restrict__ buckets,
 #pragma unroll
   for (uint32_t i = 0; i <= RL; i++) bs[i] = i <= nb ? bucket_start[key0 + i] : 0u;
   uint32_t live = 0, cross = 0;
+  const double ginv = 1.0 / ((double)K * ACC_THREADS);  // (bs / K) / ACC_THREADS = bs / (K ACC_THREADS)
 #pragma unroll
   for (uint32_t i = 0; i < RL; i++) {
     if (i < nb && bs[i + 1] != bs[i]) {
       live |= 1u << i;
-      if (cross_key[(bs[i] / K) / ACC_THREADS] == key0 + i) cross |= 1u << i;
+      if (cross_key[div_by_inv(bs[i], ginv)] == key0 + i) cross |= 1u << i;
     }
   }
   if (!live) {  // whole chunk empty (e.g. the windows above the scalars' top bit)
