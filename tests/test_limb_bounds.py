@@ -132,6 +132,34 @@ def fe_mul_2d_exact(v: int):
     return r, value_of(r)
 
 
+KD_INT, MU272 = 3021, (1 << 272) // P
+
+
+def fe_mul_d_exact(v: int):
+    """Bit-exact model of fp29.cuh fe_mul_d on the normalised representation of v (< 2^254):
+    returns (limbs, value)."""
+    a = [(v >> (LB * i)) & MASK for i in range(NL - 1)] + [v >> (LB * (NL - 1))]
+    r, c = [0] * NL, 0
+    for i in range(NL - 1):
+        c = a[i] * KD_INT + c
+        assert c < 1 << 64
+        r[i] = c & MASK
+        c >>= LB
+    c = a[NL - 1] * KD_INT + c
+    assert c < 1 << 34
+    q = ((c >> 8) * MU272) >> 32
+    assert q < 1 << 32
+    d = 0
+    for i in range(NL - 1):
+        d += r[i] - q * P29[i]
+        assert -(1 << 63) <= d < 1 << 63
+        r[i] = d & MASK
+        d >>= LB
+    r[NL - 1] = d + c - q * P29[NL - 1]
+    assert 0 <= r[NL - 1] < 1 << 32
+    return r, value_of(r)
+
+
 def fe_mul_2d(a: B) -> B:
     assert all(x <= MASK for x in a.l[:NL - 1]) and a.v < 1 << 254
     return B.normalised(3 * P)
@@ -430,6 +458,28 @@ def test_mul_2d_exact_and_bounded():
         assert all(x <= MASK for x in limbs[:NL - 1])
 
 
+def test_mul_d_exact_and_below_2p():
+    # k_prepare_points: d t = fe_mul_d(fe_mul(x + x, y + y)); the result must be normalised and
+    # < 2p like an fe_mul output (pt_madd's C and kt_neg_if's 5p - kt rely on it)
+    import random
+    rnd = random.Random(12)
+    vals = [0, 1, P - 1, P, 2 * P - 1, (1 << 254) - 1, (1 << 253), (1 << 252) - 1]
+    vals += [rnd.randrange(0, 2 * P) for _ in range(20000)] + [rnd.randrange(0, 1 << 254) for _ in range(5000)]
+    for q in range(0, KD_INT * 2 + 2, 7):  # every Barrett boundary q p of 3021 v, both sides
+        for dv in (-2, -1, 0, 1):
+            x = (q * P) // KD_INT + dv
+            if 0 <= x < 1 << 254:
+                vals.append(x)
+    for v in vals:
+        limbs, r = fe_mul_d_exact(v)
+        assert r % P == (KD_INT * v) % P
+        assert 0 <= r < 2 * P, (v, r)
+        assert all(x <= MASK for x in limbs[:NL - 1])
+    # the multiply before it: two doubled fe_mul outputs (S form, value < 4p) meet in fe_mul
+    x2 = fe_add(B.normalised(2 * P - 1), B.normalised(2 * P - 1))
+    fe_mul(x2, x2)
+
+
 def test_quad_add_bounds():
     # pt_add_quad: round 1 A | B | T1T2 | Z1Z2 on the four lanes, C = fe_mul_2d(T1T2) on lane 2,
     # then EF | GH | EH | FG -- the same operands as pt_add, through one multiply whose wide steps
@@ -532,6 +582,7 @@ REVIEWED = {
     ("fp29.cuh", "fe_sub_u"): "3dba987a0530b5b5",
     ("fp29.cuh", "fe_neg"): "a754b1a94a6b8415",
     ("fp29.cuh", "fe_mul_2d"): "b9f5c6afdcbc7ff4",
+    ("fp29.cuh", "fe_mul_d"): "be44d19d0395d3fb",
     ("fp29.cuh", "P29"): "b4babf5a3c9d7331",
     ("fp29.cuh", "K8P29"): "13315f5ba6ec470d",
     ("fp29.cuh", "K5P29"): "f3dc542f8a39d740",

@@ -311,6 +311,36 @@ __device__ __forceinline__ fe fe_mul_2d(const fe& a) {
   return r;
 }
 
+// d * a = 3021 a (mod p) with the result below 2p (the bound of an fe_mul output), for
+// k_prepare_points' d t = d x y (one fe_mul fewer than multiplying by the Montgomery form of d).
+// Limbs scaled as in fe_mul_2d, then v = 3021 a < 2^266 (a < 2^254) is reduced by q p with
+// q = floor(floor(v / 2^240) * MU272 / 2^32), MU272 = floor(2^272 / p): the two truncations
+// cost less than 0.06 of a unit, so q is floor(v / p) or one less and 0 <= v - q p < 2p.
+// Requires a normalised; returns normalised.  tests/test_limb_bounds.py models it bit-exactly.
+constexpr uint32_t KD_INT = 3021;
+constexpr uint32_t MU272 = 898642u;  // floor(2^272 / p)
+__device__ __forceinline__ fe fe_mul_d(const fe& a) {
+  fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    c = mad64(a.v[i], KD_INT, c);
+    r.v[i] = (uint32_t)c & LMASK;
+    c >>= LBITS;
+  }
+  c = mad64(a.v[NL - 1], KD_INT, c);  // v = c 2^232 + (limbs 0..7), c < 2^34
+  const uint32_t q = (uint32_t)(((c >> 8) * (uint64_t)MU272) >> 32);
+  int64_t d = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    d += (int64_t)r.v[i] - (int64_t)q * (int64_t)P29[i];
+    r.v[i] = (uint32_t)d & LMASK;
+    d >>= LBITS;  // arithmetic: borrows propagate
+  }
+  r.v[NL - 1] = (uint32_t)(d + (int64_t)c - (int64_t)q * (int64_t)P29[NL - 1]);
+  return r;
+}
+
 // Carry-propagate so limbs 0..7 are < 2^29 (value unchanged).
 __device__ __forceinline__ void fe_norm(fe& a) {
 #pragma unroll

@@ -102,9 +102,6 @@ constexpr uint32_t PT_FMT_WIRE = 0, PT_FMT_XY = 1, PT_FMT_XYZ = 2;
 __host__ __device__ constexpr uint32_t pt_fmt_slots(uint32_t fmt) {  // 16-B slots per input point
   return fmt == PT_FMT_XY ? 4u : fmt == PT_FMT_XYZ ? 6u : 8u;
 }
-// Montgomery form of 4d: d t = 4d (x/2)(y/2) from the halved coordinates.
-__device__ constexpr uint32_t K4D29[NL] = {531568572u, 449839103u, 184174685u, 15704447u, 1165364u,
-                                           393938084u, 340476652u, 106785266u, 592681u};
 
 // blockIdx.y = MSM of the batch: its wire points come from wires.p[y], its records go to
 // pts[y n ..).
@@ -178,7 +175,8 @@ extern "C" __global__ void __launch_bounds__(PP_THREADS) k_prepare_points(BatchP
     x = fe_mul(fe_to_mont(fe_from_words_le(xw)), zh);
     y = fe_mul(fe_to_mont(fe_from_words_le(yw)), zh);
   }
-  const fe kt = fe_mul(fe_mul(x, y), fe_const(K4D29));  // d x y = 4d (x/2)(y/2)
+  // d x y: (2 (x/2)) (2 (y/2)) = x y in Montgomery form (S x S operands), then d by limb scaling
+  const fe kt = fe_mul_d(fe_mul(fe_add(x, x), fe_add(y, y)));
   fe ymx = fe_sub(y, x);
   fe ypx = fe_add_n(y, x);
   uint32_t rec[32];  // layout: msm_dev.h PRE_WORDS
